@@ -1,0 +1,713 @@
+// galaxy-deconv_amd: MI355X-native spectral engine for unrolled PnP-ADMM deconvolution.
+//
+// Three streaming kernels per 2D spectral round trip, all fp32:
+//   k_row_fwd  (RF)  : per block RW rows of one galaxy.  Two real images p, w are packed as one
+//                      complex line c = p + i w, length-L FFT along the row inside one wave, split
+//                      into the two half spectra (kx = 0..L/2), stored TRANSPOSED to the
+//                      workspace T[N][2][K][L] (K = L/2+1) so the column pass reads contiguous
+//                      columns.  Mode-specific producers fuse the preceding elementwise work
+//                      (z - u1, PSF placement + circular shift, max(y,0)/alpha, ...).
+//   k_col      (C)  : per line one (galaxy, kx) column of both images: column FFTs, the fused
+//                      spectral operator (X-update divide, Wiener divide, OTF capture, conv
+//                      multiply), inverse column FFTs, stored back in place.
+//   k_row_inv  (RI) : per block RW rows: Hermitian extension of the two half spectra packed as
+//                      R + iS, inverse row FFT (Re = r, Im = s), and the fused elementwise sink
+//                      (dual updates, V step, next-iteration denoiser input, outputs).
+//   k_row_invfwd (RIF): RI + a pointwise nonlinearity + RF of the result in one kernel (clamp in
+//                      init_l2, Richardson-Lucy ratio / multiplicative update).
+//
+// Reference mapping (paths relative to the reference root):
+//   psf_to_otf          utils/utils_torch.py:79-92      -> RF_PSF*, C_OTF*
+//   conv_fft_batch      utils/utils_torch.py:46-50      -> RF_ONE, C_CONV[C], RI_OUT1
+//   init_l2             models/Unrolled_ADMM.py:170-175 -> RF_PSF_Y, C_OTF_INIT, RIF_CLAMP, C_CONV, RI_INIT
+//   ADMM loop body      models/Unrolled_ADMM.py:199-214 -> RF_ITER, C_ITER, RI_ITER
+//   Wiener.forward      models/Wiener.py:10-20          -> RF_PSF_RAW, C_WIENER, RI_OUT1
+//   Richard_Lucy.forward models/Richard_Lucy.py:10-24   -> RF_PSF_YP, C_OTF_CONV, RIF_RL_RATIO,
+//                                                          C_CONVC, RIF_RL_UPDATE / RI_RL_FINAL, C_CONV
+//
+// ADMM state carried between iterations (all [N,1,L,L] fp32): u1, w = v - u2, zin (denoiser input)
+// plus y and the half-spectrum OTF.  u2 and v are never stored: u2_{n+1} = Hx_{n+1} - w_n and
+// v_{n+1} - u2_{n+1} is all the next X-update needs (algebraically identical to :207-213).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gdeconv.h"
+#include "gd_fft.hpp"
+
+namespace gd {
+
+// ---------------------------------------------------------------- per-galaxy scalar views
+struct GalScalar {
+    const float* p;
+    long long stride;  // elements between galaxies; 0 = broadcast
+    __device__ __forceinline__ float operator()(int g) const { return p[(long long)g * stride]; }
+};
+
+struct Args {
+    int N;                 // galaxies in this launch
+    float2* T;             // workspace spectra [N][2][K][L]
+    float2* otf;           // half-spectrum OTF [N][K][L] (read or written depending on mode)
+    const float* y;        // raw observation [N][L][L]
+    const float* psf;      // [*, h, h]
+    long long psf_gstride; // elements between galaxies' PSFs (0 = one shared PSF)
+    int h;                 // PSF side (even, <= L)
+    const float* a0;       // mode inputs
+    const float* a1;
+    const float* a2;
+    float* o0;             // mode outputs
+    float* o1;
+    float* o2;
+    GalScalar alpha, rho1, rho2, rho2n;
+    int llh;               // GD_LLH_GAUSSIAN / GD_LLH_POISSON
+    int last;              // final ADMM iteration: write x (times alpha for Poisson) to o2
+};
+
+enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO };
+enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV };
+enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
+enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
+
+constexpr int rows_per_block(int lpb, int L) {
+    int rw = lpb < L ? lpb : L;
+    while (L % rw) --rw;
+    return rw;
+}
+
+template <int L>
+struct Geo {
+    static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2;
+    static constexpr int K = L / 2 + 1;
+    static constexpr int LPB = 256 / F1;               // lines per 256-thread block
+    static constexpr int RW = rows_per_block(LPB, L);  // rows per row-kernel block (divides L)
+    static constexpr int ROW_THREADS = RW * F1;
+    static constexpr int RLD = L + 2;                  // row buffer leading dim (bank spread)
+    static constexpr int XCH = xch_elems<L>();
+    static constexpr int ROW_LDS = (RW * RLD > LPB * XCH) ? RW * RLD : LPB * XCH;
+    static constexpr int COL_LDS = LPB * XCH;
+    static_assert(L % RW == 0, "rows per block must divide L");
+};
+
+__device__ __forceinline__ size_t tidx(int g, int img, int k, int row, int K, int L) {
+    return ((size_t)(g * 2 + img) * K + k) * L + row;
+}
+
+__device__ __forceinline__ float shifted_psf(const Args& a, int g, int r, int c, int L) {
+    const int c0 = a.h >> 1;
+    int i = r + c0, jj = c + c0;
+    if (i >= L) i -= L;
+    if (jj >= L) jj -= L;
+    if (i >= a.h || jj >= a.h) return 0.0f;
+    return a.psf[(long long)g * a.psf_gstride + (long long)i * a.h + jj];
+}
+
+// V step (runtime classes, models/Unrolled_ADMM.py:326-328 and :335-336); yp = max(y, 0)
+__device__ __forceinline__ float v_step(int llh, float vt, float yp, float rho2, float alpha) {
+    if (llh == GD_LLH_POISSON) {
+        const float t1 = rho2 * vt - alpha;
+        return 0.5f * (1.0f / rho2) * (-t1 + sqrtf(t1 * t1 + 4.0f * yp * rho2));
+    }
+    return (rho2 * vt + yp / alpha) / (1.0f + rho2);
+}
+
+// ---------------------------------------------------------------- row-side building blocks
+// Split packed row spectra C = FFT(p + i w) held in the row buffer into P and W half spectra
+// and store them transposed: T[g][img][k][row].
+template <int L, bool TWO>
+__device__ __forceinline__ void split_store(const Args& a, const float2* rowbuf, int g, int row0,
+                                            int tid, int nthreads) {
+    using G = Geo<L>;
+    for (int idx = tid; idx < G::K * G::RW; idx += nthreads) {
+        const int k = idx / G::RW, rr = idx - k * G::RW;
+        const float2 C = rowbuf[rr * G::RLD + k];
+        const float2 D = rowbuf[rr * G::RLD + (k == 0 ? 0 : L - k)];
+        // P = (C + conj D)/2 ; W = (C - conj D)/(2i)
+        a.T[tidx(g, 0, k, row0 + rr, G::K, L)] = make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));
+        if (TWO) a.T[tidx(g, 1, k, row0 + rr, G::K, L)] = make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+    }
+}
+
+// Load the two half spectra of rows [row0, row0+RW) and build the Hermitian-extended packed
+// spectrum D = R + i S over kx in [0, L) in the row buffer.
+template <int L, bool TWO>
+__device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g, int row0, int tid,
+                                            int nthreads) {
+    using G = Geo<L>;
+    for (int idx = tid; idx < G::K * G::RW; idx += nthreads) {
+        const int k = idx / G::RW, rr = idx - k * G::RW;
+        float2 R = a.T[tidx(g, 0, k, row0 + rr, G::K, L)];
+        float2 S = TWO ? a.T[tidx(g, 1, k, row0 + rr, G::K, L)] : make_float2(0.f, 0.f);
+        const bool self = (k == 0) || (2 * k == L);  // self-conjugate bins: keep real parts only
+        if (self) {
+            R.y = 0.f;
+            S.y = 0.f;
+        }
+        rowbuf[rr * G::RLD + k] = make_float2(R.x - S.y, R.y + S.x);
+        if (!self) rowbuf[rr * G::RLD + (L - k)] = make_float2(R.x + S.y, S.x - R.y);
+    }
+}
+
+// ---------------------------------------------------------------- RF: row forward
+template <int L, int MODE>
+__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_fwd(Args a) {
+    using G = Geo<L>;
+    constexpr int F1 = G::F1, F2 = G::F2;
+    constexpr bool TWO = (MODE != RF_PSF && MODE != RF_ONE);
+    __shared__ float2 tw[L];
+    __shared__ float2 lds[G::ROW_LDS];
+    const int tid = threadIdx.x;
+    const int blocks_per_g = L / G::RW;
+    const int g = blockIdx.x / blocks_per_g;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int line = tid / F1, j = tid - line * F1;
+    const int r = row0 + line;
+    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
+
+    const size_t rbase = ((size_t)g * L + r) * L;
+    float2 v[F2];
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int c = j + F1 * s;
+        const size_t pix = rbase + c;
+        float p = 0.f, w = 0.f;
+        if constexpr (MODE == RF_ITER) {
+            p = a.a0[pix] - a.a1[pix];  // z - u1
+            w = a.a2[pix];              // v - u2
+        } else if constexpr (MODE == RF_PSF_Y) {
+            p = shifted_psf(a, g, r, c, L);
+            w = fmaxf(a.y[pix], 0.f) / a.alpha(g);
+        } else if constexpr (MODE == RF_PSF_YP) {
+            p = shifted_psf(a, g, r, c, L);
+            w = fmaxf(a.y[pix], 0.f);
+            a.o0[pix] = w;  // Richardson-Lucy x0 = max(y, 0)
+        } else if constexpr (MODE == RF_PSF_RAW) {
+            p = shifted_psf(a, g, r, c, L);
+            w = a.y[pix];
+        } else if constexpr (MODE == RF_PSF) {
+            p = shifted_psf(a, g, r, c, L);
+        } else if constexpr (MODE == RF_ONE) {
+            p = a.a0[pix];
+        } else {
+            p = a.a0[pix];
+            w = a.a1[pix];
+        }
+        v[s] = make_float2(p, w);
+    }
+    __syncthreads();  // twiddles
+    line_fft<L, false>(v, j, lds + line * G::XCH, tw);
+    __syncthreads();  // exchange area -> row buffer
+#pragma unroll
+    for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
+    __syncthreads();
+    split_store<L, TWO>(a, lds, g, row0, tid, G::ROW_THREADS);
+}
+
+// ---------------------------------------------------------------- C: column pass
+template <int MODE>
+struct ColTraits {
+    static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
+                                 MODE == C_WIENER || MODE == C_CONV2);
+    static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
+    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD);
+    static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
+    static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2);
+    static constexpr bool FWD = (MODE != C_INV);
+};
+
+template <int L, int MODE>
+__global__ __launch_bounds__(256) void k_col(Args a) {
+    using G = Geo<L>;
+    using TR = ColTraits<MODE>;
+    constexpr int F1 = G::F1, F2 = G::F2, K = G::K;
+    __shared__ float2 tw[L];
+    __shared__ float2 xch[G::COL_LDS];
+    const int tid = threadIdx.x;
+    const int line = tid / F1, j = tid - line * F1;
+    const int f = blockIdx.x * G::LPB + line;
+    const bool valid = f < a.N * K;
+    const int fc = valid ? f : 0;
+    const int g = fc / K, kx = fc - g * K;
+    fill_twiddles<L>(tw, tid, 256);
+    float2* my = xch + line * G::XCH;
+
+    float2 P[F2], Q[F2];
+    const size_t c0 = tidx(g, 0, kx, 0, K, L), c1 = tidx(g, 1, kx, 0, K, L);
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        P[s] = a.T[c0 + j + F1 * s];
+        if constexpr (TR::IN2) Q[s] = a.T[c1 + j + F1 * s];
+    }
+    __syncthreads();  // twiddles
+    if constexpr (TR::FWD) {
+        line_fft<L, false>(P, j, my, tw);
+        if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
+    }
+    constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
+    const size_t ob = ((size_t)g * K + kx) * L;
+    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER) ? a.alpha(g) : 1.f;
+    const float r1 = (MODE == C_ITER) ? a.rho1(g) : 0.f;
+    const float r2 = (MODE == C_ITER) ? a.rho2(g) : 0.f;
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int ky = j + F1 * s;
+        float2 Hk = make_float2(0.f, 0.f);
+        if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
+        if constexpr (TR::STORE_OTF || MODE == C_WIENER) Hk = P[s];
+        if constexpr (TR::STORE_OTF) {
+            if (valid) a.otf[ob + ky] = Hk;
+        }
+        if constexpr (MODE == C_ITER) {
+            // runtime X_Update (models/Unrolled_ADMM.py:315-319):
+            //   X = (rho1 F(z-u1) + rho2 conj(H) F(v-u2)) / (rho1 |H|^2 + rho2);  HX = H X
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float lhs = r1 * HtH + r2;
+            const float2 HtW = cmulc(Q[s], Hk);
+            const float2 rhs = make_float2(r1 * P[s].x + r2 * HtW.x, r1 * P[s].y + r2 * HtW.y);
+            const float2 X = make_float2(rhs.x / lhs, rhs.y / lhs);
+            P[s] = cscale(X, inv_n);
+            Q[s] = cscale(cmul(Hk, X), inv_n);
+        } else if constexpr (MODE == C_OTF_INIT) {
+            // init_l2 (models/Unrolled_ADMM.py:170-175): conj(H) F(y/alpha) / (|H|^2 + 1/alpha)
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float lhs = HtH + 1.0f / al;
+            const float2 rhs = cmulc(Q[s], Hk);
+            P[s] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
+        } else if constexpr (MODE == C_WIENER) {
+            // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float div = HtH + 350.0f / al;
+            const float2 num = cmulc(Q[s], Hk);
+            P[s] = cscale(make_float2(num.x / div, num.y / div), inv_n);
+        } else if constexpr (MODE == C_OTF_CONV) {
+            P[s] = cscale(cmul(Q[s], Hk), inv_n);
+        } else if constexpr (MODE == C_CONV) {
+            P[s] = cscale(cmul(P[s], Hk), inv_n);
+        } else if constexpr (MODE == C_CONVC) {
+            P[s] = cscale(cmulc(P[s], Hk), inv_n);
+        } else if constexpr (MODE == C_CONV2) {
+            P[s] = cscale(cmul(P[s], Hk), inv_n);
+            Q[s] = cscale(cmul(Q[s], Hk), inv_n);
+        } else if constexpr (MODE == C_INV) {
+            P[s] = cscale(P[s], inv_n);
+        }
+    }
+    if constexpr (TR::HAS_OUT && MODE != C_FWD) {
+        line_fft<L, true>(P, j, my, tw);
+        if constexpr (TR::OUT2) line_fft<L, true>(Q, j, my, tw);
+    }
+    if (valid) {
+        if constexpr (MODE == C_FWD) {
+#pragma unroll
+            for (int s = 0; s < F2; ++s) a.T[c0 + j + F1 * s] = P[s];
+        } else if constexpr (TR::HAS_OUT) {
+#pragma unroll
+            for (int s = 0; s < F2; ++s) {
+                a.T[c0 + j + F1 * s] = P[s];
+                if constexpr (TR::OUT2) a.T[c1 + j + F1 * s] = Q[s];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- RI: row inverse + sink
+template <int MODE>
+struct RiTraits {
+    static constexpr bool TWO = (MODE == RI_ITER || MODE == RI_OUT2);
+};
+
+template <int L, int MODE>
+__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_inv(Args a) {
+    using G = Geo<L>;
+    constexpr int F1 = G::F1, F2 = G::F2;
+    __shared__ float2 tw[L];
+    __shared__ float2 lds[G::ROW_LDS];
+    const int tid = threadIdx.x;
+    const int blocks_per_g = L / G::RW;
+    const int g = blockIdx.x / blocks_per_g;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int line = tid / F1, j = tid - line * F1;
+    const int r = row0 + line;
+    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
+    gather_rows<L, RiTraits<MODE>::TWO>(a, lds, g, row0, tid, G::ROW_THREADS);
+    __syncthreads();
+    float2 v[F2];
+#pragma unroll
+    for (int s = 0; s < F2; ++s) v[s] = lds[line * G::RLD + j + F1 * s];
+    __syncthreads();  // row buffer -> exchange area
+    line_fft<L, true>(v, j, lds + line * G::XCH, tw);
+
+    const size_t rbase = ((size_t)g * L + r) * L;
+    float al = 1.f, r2n = 1.f, div = 1.f;
+    if constexpr (MODE == RI_ITER || MODE == RI_INIT) {
+        al = a.alpha(g);
+        if (!(MODE == RI_ITER && a.last)) r2n = a.rho2n(g);
+    }
+    if constexpr (MODE == RI_RL_FINAL) div = a.otf[(size_t)g * G::K * L].x;  // conv(Ht, ones) = H(0,0)
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const size_t pix = rbase + j + F1 * s;
+        const float re = v[s].x, im = v[s].y;
+        if constexpr (MODE == RI_ITER) {
+            // models/Unrolled_ADMM.py:207-213 (x = re, conv(H,x) = im)
+            const float z = a.a0[pix];
+            const float u1 = (a.o0[pix] + re) - z;     // u1 + x - z
+            const float u2 = im - a.o1[pix];           // u2 + Hx - v  (w = v - u2)
+            if (a.last) {
+                a.o2[pix] = (a.llh == GD_LLH_POISSON) ? re * al : re;
+            } else {
+                const float yp = fmaxf(a.y[pix], 0.f);
+                const float vn = v_step(a.llh, im + u2, yp, r2n, al);
+                a.o0[pix] = u1;
+                a.o1[pix] = vn - u2;
+                a.o2[pix] = re + u1;                   // next denoiser input x + u1
+            }
+        } else if constexpr (MODE == RI_INIT) {
+            // first V step with x = x0 (zin), u1 = u2 = 0: v = V(conv(H,x0) + 0, ...)
+            const float yp = fmaxf(a.y[pix], 0.f);
+            a.o1[pix] = v_step(a.llh, re + 0.0f, yp, r2n, al);
+            a.o0[pix] = 0.f;
+        } else if constexpr (MODE == RI_OUT1) {
+            a.o0[pix] = re;
+        } else if constexpr (MODE == RI_OUT2) {
+            a.o0[pix] = re;
+            a.o1[pix] = im;
+        } else if constexpr (MODE == RI_RL_FINAL) {
+            a.o0[pix] = a.o0[pix] * re / div;          // x * numerator / divisor
+        }
+    }
+}
+
+// ---------------------------------------------------------------- RIF: row inverse -> pointwise -> row forward
+template <int L, int MODE>
+__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_invfwd(Args a) {
+    using G = Geo<L>;
+    constexpr int F1 = G::F1, F2 = G::F2;
+    __shared__ float2 tw[L];
+    __shared__ float2 lds[G::ROW_LDS];
+    const int tid = threadIdx.x;
+    const int blocks_per_g = L / G::RW;
+    const int g = blockIdx.x / blocks_per_g;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int line = tid / F1, j = tid - line * F1;
+    const int r = row0 + line;
+    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
+    gather_rows<L, false>(a, lds, g, row0, tid, G::ROW_THREADS);
+    __syncthreads();
+    float2 v[F2];
+#pragma unroll
+    for (int s = 0; s < F2; ++s) v[s] = lds[line * G::RLD + j + F1 * s];
+    __syncthreads();
+    line_fft<L, true>(v, j, lds + line * G::XCH, tw);
+
+    const size_t rbase = ((size_t)g * L + r) * L;
+    float div = 1.f;
+    if constexpr (MODE == RIF_RL_UPDATE) div = a.otf[(size_t)g * G::K * L].x;
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const size_t pix = rbase + j + F1 * s;
+        const float re = v[s].x;
+        float p;
+        if constexpr (MODE == RIF_CLAMP) {
+            p = fminf(fmaxf(re, 0.f), 1.f);            // torch.clamp(x0, 0, 1)
+            a.o0[pix] = p;
+        } else if constexpr (MODE == RIF_RL_RATIO) {
+            p = fmaxf(a.y[pix], 0.f) / re;             // y / Hx
+        } else {
+            p = a.o0[pix] * re / div;                  // x * numerator / divisor
+            a.o0[pix] = p;
+        }
+        v[s] = make_float2(p, 0.f);
+    }
+    line_fft<L, false>(v, j, lds + line * G::XCH, tw);
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
+    __syncthreads();
+    split_store<L, false>(a, lds, g, row0, tid, G::ROW_THREADS);
+}
+
+// ---------------------------------------------------------------- host-side launch helpers
+thread_local std::string g_last_error;
+
+inline int fail(int code, const char* msg) {
+    g_last_error = msg;
+    return code;
+}
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+        return GD_ERR_HIP;
+    }
+    return GD_OK;
+}
+
+template <int L>
+struct Launcher {
+    using G = Geo<L>;
+    static int row_grid(int N) { return N * (L / G::RW); }
+    static int col_grid(int N) { return (N * G::K + G::LPB - 1) / G::LPB; }
+
+    template <int MODE>
+    static int rf(const Args& a, hipStream_t st) {
+        hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        return check_launch("k_row_fwd");
+    }
+    template <int MODE>
+    static int col(const Args& a, hipStream_t st) {
+        hipLaunchKernelGGL((k_col<L, MODE>), dim3(col_grid(a.N)), dim3(256), 0, st, a);
+        return check_launch("k_col");
+    }
+    template <int MODE>
+    static int ri(const Args& a, hipStream_t st) {
+        hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        return check_launch("k_row_inv");
+    }
+    template <int MODE>
+    static int rif(const Args& a, hipStream_t st) {
+        hipLaunchKernelGGL((k_row_invfwd<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        return check_launch("k_row_invfwd");
+    }
+};
+
+#define GD_TRY(x)                    \
+    do {                             \
+        int _rc = (x);               \
+        if (_rc != GD_OK) return _rc; \
+    } while (0)
+
+// Operation bodies, templated on L.
+template <int L>
+struct Ops {
+    using Lc = Launcher<L>;
+    static int psf_to_otf(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_PSF>(a, st));
+        return Lc::template col<C_OTF>(a, st);
+    }
+    static int conv(Args a, int conj, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_ONE>(a, st));
+        GD_TRY(conj ? Lc::template col<C_CONVC>(a, st) : Lc::template col<C_CONV>(a, st));
+        return Lc::template ri<RI_OUT1>(a, st);
+    }
+    static int rfft2(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_ONE>(a, st));
+        return Lc::template col<C_FWD>(a, st);
+    }
+    static int irfft2(Args a, hipStream_t st) {
+        GD_TRY(Lc::template col<C_INV>(a, st));
+        return Lc::template ri<RI_OUT1>(a, st);
+    }
+    static int admm_init(Args a, hipStream_t st) {
+        // a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
+        Args b = a;
+        GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
+        GD_TRY(Lc::template col<C_OTF_INIT>(b, st));
+        b.o0 = a.o2;  // RIF_CLAMP writes x0 -> zin
+        GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
+        GD_TRY(Lc::template col<C_CONV>(b, st));
+        return Lc::template ri<RI_INIT>(a, st);
+    }
+    static int admm_iter(Args a, hipStream_t st) {
+        // a.a0 = z, a.a1 = u1 (RF reads), a.a2 = w; RI: a.o0 = u1, a.o1 = w, a.o2 = zin / out
+        GD_TRY(Lc::template rf<RF_ITER>(a, st));
+        GD_TRY(Lc::template col<C_ITER>(a, st));
+        return Lc::template ri<RI_ITER>(a, st);
+    }
+    static int wiener(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_PSF_RAW>(a, st));
+        GD_TRY(Lc::template col<C_WIENER>(a, st));
+        return Lc::template ri<RI_OUT1>(a, st);
+    }
+    static int richardson_lucy(Args a, int n_iters, hipStream_t st) {
+        // a.o0 = x (output, also the iterate); otf kept in a.otf
+        GD_TRY(Lc::template rf<RF_PSF_YP>(a, st));
+        if (n_iters <= 0) return GD_OK;
+        GD_TRY(Lc::template col<C_OTF_CONV>(a, st));
+        for (int it = 0; it < n_iters; ++it) {
+            if (it > 0) GD_TRY(Lc::template col<C_CONV>(a, st));
+            GD_TRY(Lc::template rif<RIF_RL_RATIO>(a, st));
+            GD_TRY(Lc::template col<C_CONVC>(a, st));
+            if (it + 1 < n_iters)
+                GD_TRY(Lc::template rif<RIF_RL_UPDATE>(a, st));
+            else
+                GD_TRY(Lc::template ri<RI_RL_FINAL>(a, st));
+        }
+        return GD_OK;
+    }
+};
+
+template <template <int> class OP, typename F>
+int dispatch(int L, F&& f) {
+    switch (L) {
+        case 32: return f(OP<32>{});
+        case 48: return f(OP<48>{});
+        case 64: return f(OP<64>{});
+        case 96: return f(OP<96>{});
+        case 128: return f(OP<128>{});
+        case 256: return f(OP<256>{});
+        default: return fail(GD_ERR_UNSUPPORTED, "unsupported image size (supported: 32, 48, 64, 96, 128, 256, square)");
+    }
+}
+
+inline int check_shape(int N, int H, int W) {
+    if (N < 0) return fail(GD_ERR_ARG, "negative batch");
+    if (H != W) return fail(GD_ERR_UNSUPPORTED, "only square images are supported");
+    if (!gd_supported_size(H, W)) return fail(GD_ERR_UNSUPPORTED, "unsupported image size");
+    return GD_OK;
+}
+
+inline int check_psf(int h, int w, int H) {
+    if (h != w) return fail(GD_ERR_ARG, "psf must be square (psf_to_otf uses ker.shape[2] for both axes)");
+    if (h <= 0 || (h & 1)) return fail(GD_ERR_ARG, "psf side must be even (odd sizes fail in the reference's quadrant copy)");
+    if (h > H) return fail(GD_ERR_ARG, "psf larger than the image");
+    return GD_OK;
+}
+
+inline Args base_args(int N, void* ws, int L) {
+    Args a;
+    std::memset(&a, 0, sizeof(a));
+    a.N = N;
+    a.T = reinterpret_cast<float2*>(ws);
+    (void)L;
+    a.alpha = GalScalar{nullptr, 0};
+    a.rho1 = a.rho2 = a.rho2n = a.alpha;
+    return a;
+}
+
+}  // namespace gd
+
+using namespace gd;
+
+// ====================================================================== C ABI
+extern "C" {
+
+int gd_abi_version(void) { return GD_ABI_VERSION; }
+
+const char* gd_last_error(void) { return g_last_error.c_str(); }
+
+int gd_supported_size(int H, int W) {
+    if (H != W) return 0;
+    switch (H) {
+        case 32: case 48: case 64: case 96: case 128: case 256: return 1;
+        default: return 0;
+    }
+}
+
+size_t gd_workspace_bytes(int N, int H, int W) {
+    if (!gd_supported_size(H, W) || N <= 0) return 0;
+    const size_t K = (size_t)W / 2 + 1;
+    return (size_t)N * 2 * K * H * sizeof(float2);
+}
+
+size_t gd_otf_bytes(int N, int H, int W) {
+    if (!gd_supported_size(H, W) || N <= 0) return 0;
+    return (size_t)N * (W / 2 + 1) * H * sizeof(float2);
+}
+
+int gd_psf_to_otf(const float* psf, long long psf_gstride, int h, int w, int N, int H, int W,
+                  void* otf_half, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.otf = reinterpret_cast<float2*>(otf_half);
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::psf_to_otf(a, (hipStream_t)stream); });
+}
+
+int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out, int N, int H, int W,
+                      void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.otf = reinterpret_cast<float2*>(const_cast<void*>(otf_half));
+    a.a0 = x; a.o0 = out;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::conv(a, conj, (hipStream_t)stream); });
+}
+
+int gd_rfft2(const float* x, void* spec, int N, int H, int W, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, spec, H);  // spectrum lives in image slot 0 of a T-shaped buffer
+    a.a0 = x;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::rfft2(a, (hipStream_t)stream); });
+}
+
+int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, spec, H);
+    a.o0 = x;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::irfft2(a, (hipStream_t)stream); });
+}
+
+int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
+                 const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
+                 int llh, int N, int H, int W, void* otf_half, float* u1, float* wv, float* zin,
+                 void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H));
+    if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    a.rho2n = GalScalar{rho2, rho2_stride};
+    a.llh = llh;
+    a.otf = reinterpret_cast<float2*>(otf_half);
+    a.o0 = u1; a.o1 = wv; a.o2 = zin;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
+}
+
+int gd_admm_iter(const float* y, const void* otf_half, const float* z, float* u1, float* wv,
+                 float* zin_or_out, const float* alpha, long long alpha_stride, const float* rho1,
+                 long long rho1_stride, const float* rho2, long long rho2_stride,
+                 const float* rho2_next, long long rho2_next_stride, int llh, int last, int N, int H,
+                 int W, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
+    if (N == 0) return GD_OK;
+    if (!last && rho2_next == nullptr) return fail(GD_ERR_ARG, "rho2_next required unless last");
+    Args a = base_args(N, ws, H);
+    a.y = y;
+    a.otf = reinterpret_cast<float2*>(const_cast<void*>(otf_half));
+    a.a0 = z; a.a1 = u1; a.a2 = wv;
+    a.o0 = u1; a.o1 = wv; a.o2 = zin_or_out;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    a.rho1 = GalScalar{rho1, rho1_stride};
+    a.rho2 = GalScalar{rho2, rho2_stride};
+    a.rho2n = GalScalar{rho2_next ? rho2_next : rho2, rho2_next ? rho2_next_stride : rho2_stride};
+    a.llh = llh;
+    a.last = last;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter(a, (hipStream_t)stream); });
+}
+
+int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+              long long alpha_stride, float* x, int N, int H, int W, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    a.o0 = x;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::wiener(a, (hipStream_t)stream); });
+}
+
+int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
+                       float* x, int N, int H, int W, void* otf_half, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H));
+    if (n_iters < 0) return fail(GD_ERR_ARG, "n_iters must be >= 0");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.otf = reinterpret_cast<float2*>(otf_half);
+    a.o0 = x;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
+}
+
+}  // extern "C"

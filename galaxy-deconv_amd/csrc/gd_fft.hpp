@@ -1,0 +1,225 @@
+// Device-side FFT building blocks for gfx950 (CDNA4), fp32.
+//
+//  * DFT<N, INV>      : in-register mixed-radix (2/3/4) Cooley-Tukey on N complex values, every
+//                       twiddle a compile-time constant (computed in double, rounded once).
+//  * line_fft<L, INV> : length-L complex FFT spread over F1 lanes of ONE wave (the "line"), each
+//                       lane holding F2 = L/F1 points.  Four-step: DFT-F2 in registers, twiddle
+//                       W_L^{n1 k1} from an LDS table, one LDS transpose inside the wave, DFT-F1
+//                       in registers.  Lane j holds x[j + F1*r] (r = 0..F2-1) on entry and
+//                       X[j + F1*r] on exit, so a forward transform, a pointwise spectral op and an
+//                       inverse transform chain with no extra data movement.
+//  Requirements: F1 | F2 (so stage B is balanced), F1 <= 64, line lanes contiguous in one wave.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+#include <utility>
+
+namespace gd {
+
+// ---------------------------------------------------------------- compile-time trigonometry
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+constexpr double cx_sin(double x) {  // |x| <= pi; Taylor to far below double eps
+    double term = x, sum = x;
+    for (int i = 1; i < 40; ++i) {
+        term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double cx_cos(double x) {
+    double term = 1.0, sum = 1.0;
+    for (int i = 1; i < 40; ++i) {
+        term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+        sum += term;
+    }
+    return sum;
+}
+// W_N^m = exp(-+2 pi i m / N) (forward: minus), angle reduced to [-pi, pi] before the series.
+template <int N, int M, bool INV>
+struct Twiddle {
+    static constexpr int m = ((M % N) + N) % N;
+    static constexpr int mr = (2 * m > N) ? m - N : m;  // in [-N/2, N/2]
+    static constexpr double ang = (INV ? 2.0 : -2.0) * kPi * double(mr) / double(N);
+    static constexpr float re = float(cx_cos(ang));
+    static constexpr float im = float(cx_sin(ang));
+};
+
+// ---------------------------------------------------------------- complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// multiply by -i (forward) or +i (inverse)
+template <bool INV>
+__device__ __forceinline__ float2 mul_mi(float2 a) {
+    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+
+template <int N, int M, bool INV>
+__device__ __forceinline__ float2 twmul(float2 v) {
+    constexpr int m = ((M % N) + N) % N;
+    if constexpr (m == 0) {
+        return v;
+    } else if constexpr (2 * m == N) {
+        return make_float2(-v.x, -v.y);
+    } else if constexpr (4 * m == N) {
+        return mul_mi<INV>(v);
+    } else if constexpr (4 * m == 3 * N) {
+        return mul_mi<!INV>(v);
+    } else {
+        return cmul(v, make_float2(Twiddle<N, M, INV>::re, Twiddle<N, M, INV>::im));
+    }
+}
+
+// ---------------------------------------------------------------- static_for
+template <int I, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, E>(f);
+    }
+}
+
+// ---------------------------------------------------------------- in-register DFTs
+constexpr int first_factor(int n) { return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : 3); }
+
+template <int N, bool INV>
+struct DFT {
+    static constexpr int A = first_factor(N);
+    static constexpr int B = N / A;
+    static_assert(A * B == N, "unsupported DFT size");
+    // N = A*B, n = A*n2 + n1, k = k1 + B*k2
+    __device__ __forceinline__ static void run(float2 (&x)[N]) {
+        float2 t[A][B];
+        static_for<0, A>([&](auto n1c) {
+            constexpr int n1 = decltype(n1c)::value;
+            float2 y[B];
+            static_for<0, B>([&](auto n2c) { y[decltype(n2c)::value] = x[A * decltype(n2c)::value + n1]; });
+            DFT<B, INV>::run(y);
+            static_for<0, B>([&](auto k1c) {
+                constexpr int k1 = decltype(k1c)::value;
+                t[n1][k1] = twmul<N, n1 * k1, INV>(y[k1]);
+            });
+        });
+        static_for<0, B>([&](auto k1c) {
+            constexpr int k1 = decltype(k1c)::value;
+            float2 z[A];
+            static_for<0, A>([&](auto n1c) { z[decltype(n1c)::value] = t[decltype(n1c)::value][k1]; });
+            DFT<A, INV>::run(z);
+            static_for<0, A>([&](auto k2c) { x[k1 + B * decltype(k2c)::value] = z[decltype(k2c)::value]; });
+        });
+    }
+};
+
+template <bool INV>
+struct DFT<1, INV> {
+    __device__ __forceinline__ static void run(float2 (&)[1]) {}
+};
+
+template <bool INV>
+struct DFT<2, INV> {
+    __device__ __forceinline__ static void run(float2 (&x)[2]) {
+        const float2 a = x[0], b = x[1];
+        x[0] = cadd(a, b);
+        x[1] = csub(a, b);
+    }
+};
+
+template <bool INV>
+struct DFT<3, INV> {
+    __device__ __forceinline__ static void run(float2 (&x)[3]) {
+        constexpr float s3 = 0.866025403784438646763723170752936183f;  // sqrt(3)/2
+        const float2 t1 = cadd(x[1], x[2]);
+        const float2 t2 = make_float2(x[0].x - 0.5f * t1.x, x[0].y - 0.5f * t1.y);
+        const float2 d = csub(x[1], x[2]);
+        // forward: X1 = t2 - i s3 d ; X2 = t2 + i s3 d
+        const float2 e = mul_mi<INV>(cscale(d, s3));
+        x[0] = cadd(x[0], t1);
+        x[1] = cadd(t2, e);
+        x[2] = csub(t2, e);
+    }
+};
+
+template <bool INV>
+struct DFT<4, INV> {
+    __device__ __forceinline__ static void run(float2 (&x)[4]) {
+        const float2 a = cadd(x[0], x[2]), b = csub(x[0], x[2]);
+        const float2 c = cadd(x[1], x[3]), d = mul_mi<INV>(csub(x[1], x[3]));
+        x[0] = cadd(a, c);
+        x[2] = csub(a, c);
+        x[1] = cadd(b, d);
+        x[3] = csub(b, d);
+    }
+};
+
+// ---------------------------------------------------------------- line plans
+template <int L>
+struct Plan;
+template <> struct Plan<32>  { static constexpr int F1 = 4,  F2 = 8;  };
+template <> struct Plan<48>  { static constexpr int F1 = 4,  F2 = 12; };
+template <> struct Plan<64>  { static constexpr int F1 = 8,  F2 = 8;  };
+template <> struct Plan<96>  { static constexpr int F1 = 4,  F2 = 24; };
+template <> struct Plan<128> { static constexpr int F1 = 8,  F2 = 16; };
+template <> struct Plan<256> { static constexpr int F1 = 16, F2 = 16; };
+
+// LDS floats2 needed per line for the in-wave transpose (row pad of one element).
+template <int L>
+constexpr int xch_elems() { return Plan<L>::F1 * (Plan<L>::F2 + 1); }
+
+// Memory ordering for an exchange whose lanes all sit in ONE wave: LDS requests of a wave are
+// processed in order, so only the compiler needs fencing.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Twiddle table W_L^m = exp(-2 pi i m / L), m in [0, L), computed in double, rounded once.
+template <int L>
+__device__ __forceinline__ void fill_twiddles(float2* tw, int tid, int nthreads) {
+    for (int m = tid; m < L; m += nthreads) {
+        double s, c;
+        sincospi(-2.0 * double(m) / double(L), &s, &c);
+        tw[m] = make_float2(float(c), float(s));
+    }
+}
+
+// Length-L FFT over the F1 lanes of a line.  v[r] = x[j + F1*r] in, X[j + F1*r] out.
+// xch: this line's private LDS exchange area (xch_elems<L>() float2); tw: twiddle table.
+template <int L, bool INV>
+__device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2* xch, const float2* tw) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, M = F2 / F1, LD = F2 + 1;
+    static_assert(F2 % F1 == 0, "line plan needs F1 | F2");
+    // stage A: DFT-F2 over n2 (lane j = n1), then twiddle W_L^{n1 k1}
+    DFT<F2, INV>::run(v);
+#pragma unroll
+    for (int k1 = 1; k1 < F2; ++k1) {
+        float2 w = tw[j * k1];  // j*k1 <= (F1-1)(F2-1) < L: no wrap
+        if (INV) w.y = -w.y;
+        v[k1] = cmul(v[k1], w);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v[k1];
+    wave_lds_sync();
+    // stage B: lane j takes k1 = j + F1*m, all n1; DFT-F1 over n1
+#pragma unroll
+    for (int mm = 0; mm < M; ++mm) {
+        float2 z[F1];
+#pragma unroll
+        for (int n1 = 0; n1 < F1; ++n1) z[n1] = xch[n1 * LD + j + F1 * mm];
+        DFT<F1, INV>::run(z);
+#pragma unroll
+        for (int k2 = 0; k2 < F1; ++k2) v[mm + M * k2] = z[k2];
+    }
+    wave_lds_sync();  // the area may be rewritten by the next line_fft of this wave
+}
+
+}  // namespace gd

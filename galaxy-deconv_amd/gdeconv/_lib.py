@@ -1,0 +1,73 @@
+"""ctypes binding of ``libgdeconv.so`` (the C ABI declared in ``include/gdeconv.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``hipcc --offload-arch=gfx950``).
+There is no fallback: if the library is missing or fails to load, every engine call raises.
+``torch`` is imported first so that the process's single HIP runtime is torch's
+``libamdhip64.so.7`` (the library's NEEDED entry resolves to the already-loaded soname).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before dlopen of the engine)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgdeconv.so")
+
+GD_OK = 0
+GD_LLH = {"Gaussian": 0, "Poisson": 1}
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_LL = ctypes.c_longlong
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/gdeconv.h exactly (checked by tests/test_abi.py)
+SIGNATURES = {
+    "gd_abi_version": (_I, []),
+    "gd_last_error": (ctypes.c_char_p, []),
+    "gd_supported_size": (_I, [_I, _I]),
+    "gd_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "gd_otf_bytes": (_SZ, [_I, _I, _I]),
+    "gd_psf_to_otf": (_I, [_P, _LL, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "gd_conv_fft_batch": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _P]),
+    "gd_rfft2": (_I, [_P, _P, _I, _I, _I, _P]),
+    "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
+    "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gd_admm_iter": (_I, [_P, _P, _P, _P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I,
+                          _P, _P]),
+    "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
+    "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
+}
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load (once) and return the engine library; raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EngineError(f"HIP engine library not found at {path}: build it with "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gd_abi_version() != 1:
+        raise EngineError("libgdeconv.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != GD_OK:
+        msg = load().gd_last_error()
+        raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+__all__ = ["load", "check", "EngineError", "SIGNATURES", "LIB_PATH", "GD_LLH"]

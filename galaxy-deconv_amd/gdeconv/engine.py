@@ -1,0 +1,210 @@
+"""Tensor-level entry points of the HIP spectral engine (torch tensors in, torch tensors out).
+
+Every function requires ROCm device tensors and enqueues the HIP kernels on torch's current
+stream through the C ABI (``include/gdeconv.h``); nothing here computes on the CPU, and a missing
+library raises (``gdeconv._lib.EngineError``).
+
+Layouts: images fp32 [N,1,H,W] contiguous (NCHW, C=1, as in the reference); the OTF is the
+half spectrum stored transposed, complex64 [N, W//2+1, H] (``otf[g, kx, ky]``).
+"""
+import torch
+
+from . import _lib
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("gdeconv runs on ROCm devices only: move tensors to 'cuda' "
+                             "(the reference CPU path is not part of this engine)")
+
+
+def _img(t, name):
+    if t.dim() != 4 or t.shape[1] != 1:
+        raise ValueError(f"{name} must be [N,1,H,W], got {tuple(t.shape)}")
+    return t.float().contiguous()
+
+
+def _galaxy_scalar(t, N, name):
+    """(tensor, stride) for a per-galaxy scalar given as [N,1,1,1], [N] or a 1-element tensor."""
+    if not torch.is_tensor(t):
+        t = torch.tensor([float(t)], device="cuda")
+    t = t.float().contiguous().reshape(-1)
+    if t.numel() == N:
+        return t, 1
+    if t.numel() == 1:
+        return t, 0
+    raise ValueError(f"{name} must have 1 or N={N} elements, got {t.numel()}")
+
+
+def _psf(k, N, H, name="psf"):
+    if k.dim() != 4 or k.shape[1] != 1:
+        raise ValueError(f"{name} must be [N,1,h,w], got {tuple(k.shape)}")
+    k = k.float().contiguous()
+    if k.shape[0] not in (1, N):
+        raise ValueError(f"{name} batch must be 1 or N={N}")
+    gstride = 0 if k.shape[0] == 1 and N != 1 else k.shape[2] * k.shape[3]
+    return k, gstride
+
+
+_WS = {}
+
+
+def workspace(N, H, W, device):
+    """Per-device cached workspace of gd_workspace_bytes(N, H, W) bytes (grown on demand)."""
+    nbytes = int(_lib.load().gd_workspace_bytes(N, H, W))
+    if nbytes == 0:
+        raise ValueError(f"unsupported image size {H}x{W} (supported: square 32,48,64,96,128,256)")
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def empty_otf(N, H, W, device):
+    return torch.empty(N, W // 2 + 1, H, dtype=torch.complex64, device=device)
+
+
+def supported(H, W):
+    return bool(_lib.load().gd_supported_size(H, W))
+
+
+def psf_to_otf_half(psf, N, H, W):
+    """Half-spectrum OTF [N, W//2+1, H] of ``psf_to_otf`` (utils/utils_torch.py:79-92)."""
+    _require_device(psf)
+    lib = _lib.load()
+    k, gs = _psf(psf, N, H)
+    otf = empty_otf(N, H, W, k.device)
+    ws = workspace(N, H, W, k.device)
+    _lib.check(lib.gd_psf_to_otf(k.data_ptr(), gs, k.shape[2], k.shape[3], N, H, W, otf.data_ptr(),
+                                 ws.data_ptr(), _stream()), "gd_psf_to_otf")
+    return otf
+
+
+def conv_half(otf_half, x, conj=False):
+    """``conv_fft_batch(H, x)`` (utils/utils_torch.py:46-50) with H given as a half-spectrum OTF."""
+    _require_device(otf_half, x)
+    lib = _lib.load()
+    x = _img(x, "x")
+    N, _, H, W = x.shape
+    otf_half = otf_half.contiguous()
+    out = torch.empty_like(x)
+    ws = workspace(N, H, W, x.device)
+    _lib.check(lib.gd_conv_fft_batch(otf_half.data_ptr(), int(conj), x.data_ptr(), out.data_ptr(), N, H, W,
+                                     ws.data_ptr(), _stream()), "gd_conv_fft_batch")
+    return out
+
+
+def rfft2_half(x):
+    """Half spectrum of real images, complex64 [N, W//2+1, H] (transposed), unnormalised."""
+    _require_device(x)
+    lib = _lib.load()
+    x = _img(x, "x")
+    N, _, H, W = x.shape
+    K = W // 2 + 1
+    spec = torch.empty(N, 2, K, H, dtype=torch.complex64, device=x.device)
+    _lib.check(lib.gd_rfft2(x.data_ptr(), spec.data_ptr(), N, H, W, _stream()), "gd_rfft2")
+    return spec[:, 0].contiguous()
+
+
+def irfft2_half(spec, H, W):
+    """Inverse of ``rfft2_half`` (normalised by 1/(H W)), fp32 [N,1,H,W]."""
+    _require_device(spec)
+    lib = _lib.load()
+    N, K = spec.shape[0], W // 2 + 1
+    buf = torch.zeros(N, 2, K, H, dtype=torch.complex64, device=spec.device)
+    buf[:, 0] = spec
+    out = torch.empty(N, 1, H, W, dtype=torch.float32, device=spec.device)
+    _lib.check(lib.gd_irfft2(buf.data_ptr(), out.data_ptr(), N, H, W, _stream()), "gd_irfft2")
+    return out
+
+
+def wiener(y, psf, alpha):
+    """models/Wiener.py:10-20 on the HIP engine."""
+    _require_device(y, psf, alpha)
+    lib = _lib.load()
+    y = _img(y, "y")
+    N, _, H, W = y.shape
+    k, gs = _psf(psf, N, H)
+    al, al_s = _galaxy_scalar(alpha, N, "alpha")
+    out = torch.empty_like(y)
+    ws = workspace(N, H, W, y.device)
+    _lib.check(lib.gd_wiener(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
+                             out.data_ptr(), N, H, W, ws.data_ptr(), _stream()), "gd_wiener")
+    return out
+
+
+def richardson_lucy(y, psf, n_iters):
+    """models/Richard_Lucy.py:10-24 on the HIP engine."""
+    _require_device(y, psf)
+    lib = _lib.load()
+    y = _img(y, "y")
+    N, _, H, W = y.shape
+    k, gs = _psf(psf, N, H)
+    out = torch.empty_like(y)
+    otf = empty_otf(N, H, W, y.device)
+    ws = workspace(N, H, W, y.device)
+    _lib.check(lib.gd_richardson_lucy(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], int(n_iters),
+                                      out.data_ptr(), N, H, W, otf.data_ptr(), ws.data_ptr(), _stream()),
+               "gd_richardson_lucy")
+    return out
+
+
+class ADMMState:
+    """Device state of one unrolled-ADMM forward: u1, w = v - u2, zin (next denoiser input), OTF."""
+
+    def __init__(self, y, psf, alpha, llh):
+        _require_device(y, psf, alpha)
+        self.lib = _lib.load()
+        self.y = _img(y, "y")
+        self.N, _, self.H, self.W = self.y.shape
+        self.psf, self.psf_gs = _psf(psf, self.N, self.H)
+        self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha")
+        if llh not in _lib.GD_LLH:
+            raise ValueError("llh must be 'Gaussian' or 'Poisson'")
+        self.llh = _lib.GD_LLH[llh]
+        dev = self.y.device
+        self.u1 = torch.empty_like(self.y)
+        self.wv = torch.empty_like(self.y)
+        self.zin = torch.empty_like(self.y)
+        self.otf = empty_otf(self.N, self.H, self.W, dev)
+        self.ws = workspace(self.N, self.H, self.W, dev)
+
+    def init(self, rho2_first):
+        """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; rho2_first = (tensor, stride)."""
+        r2, r2s = rho2_first
+        k = self.psf
+        _lib.check(self.lib.gd_admm_init(
+            self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
+            self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.otf.data_ptr(),
+            self.u1.data_ptr(), self.wv.data_ptr(), self.zin.data_ptr(), self.ws.data_ptr(), _stream()),
+            "gd_admm_init")
+
+    def step(self, z, rho1, rho2, rho2_next, out=None):
+        """One loop body (models/Unrolled_ADMM.py:207-213) after the denoiser returned ``z``.
+        ``rho*`` are (tensor, stride) views; ``rho2_next`` None marks the last iteration, whose x
+        (times alpha for Poisson) goes to ``out``."""
+        z = z.float().contiguous()
+        if z.shape != self.y.shape:
+            raise ValueError(f"denoiser returned {tuple(z.shape)}, expected {tuple(self.y.shape)}")
+        last = rho2_next is None
+        dst = out if last else self.zin
+        r1, r1s = rho1
+        r2, r2s = rho2
+        rn, rns = (rho2_next if rho2_next is not None else (None, 0))
+        _lib.check(self.lib.gd_admm_iter(
+            self.y.data_ptr(), self.otf.data_ptr(), z.data_ptr(), self.u1.data_ptr(), self.wv.data_ptr(),
+            dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s, r1.data_ptr(), r1s, r2.data_ptr(), r2s,
+            None if rn is None else rn.data_ptr(), rns, self.llh, int(last), self.N, self.H, self.W,
+            self.ws.data_ptr(), _stream()), "gd_admm_iter")
+        return dst
+
+
+__all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
+           "ADMMState", "workspace", "empty_otf", "supported"]

@@ -1,0 +1,150 @@
+"""Host-side networks of the unrolled ADMM: the ResUNet denoiser (Z step) and the rho-predicting SubNet.
+
+These stay in PyTorch-ROCm (MIOpen fp32 convolutions) per the north star; only the spectral ADMM
+path is HIP.  The module *trees* are laid out so that ``state_dict`` keys are identical to the
+reference checkpoints (98 keys for ``Unrolled_ADMM``):
+
+* ``ResUNet``   mirrors ``models/ResUNet.py:7-42`` + ``models/resnet_basicblock.py:21-87``
+  (head conv, 3 x [2 ResBlocks + 2x2 stride conv], body 2 ResBlocks, 3 x [2x2 conv-transpose +
+  2 ResBlocks], tail conv; no bias, no norm; replicate-pad to a multiple of 8, additive skips).
+* ``SubNet``    mirrors ``models/Unrolled_ADMM.py:59-90`` (|FFT(pad128(psf))|^2 -> 4 x
+  [maxpool + 2 x (conv3x3+BN+ReLU)] -> MLP(1025, 64, 64, 2n) -> Softplus + 1e-6).
+
+Key layout notes (the reference builds these with a ``sequential`` helper that flattens nested
+Sequentials and returns a bare module for a single element):
+  m_head / m_tail            -> bare Conv2d                         (keys ``m_head.weight``)
+  m_downK                    -> Sequential(ResBlock, ResBlock, Conv2d(k2,s2))  (``m_down1.2.weight``)
+  m_body                     -> Sequential(ResBlock, ResBlock)
+  m_upK                      -> Sequential(ConvTranspose2d(k2,s2), ResBlock, ResBlock)
+  ResBlock.res               -> Sequential(Conv2d, ReLU, Conv2d)    (``res.0.weight``, ``res.2.weight``)
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class ResBlock(nn.Module):
+    """x + conv(relu(conv(x))), 3x3, no bias (``resnet_basicblock.py:47-59`` with mode 'CRC')."""
+
+    def __init__(self, channels):
+        super().__init__()
+        self.res = nn.Sequential(
+            nn.Conv2d(channels, channels, 3, 1, 1, bias=False),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(channels, channels, 3, 1, 1, bias=False),
+        )
+
+    def forward(self, x):
+        return x + self.res(x)
+
+
+def _down(cin, cout, nb):
+    return nn.Sequential(*[ResBlock(cin) for _ in range(nb)],
+                         nn.Conv2d(cin, cout, 2, 2, 0, bias=False))
+
+
+def _up(cin, cout, nb):
+    return nn.Sequential(nn.ConvTranspose2d(cin, cout, 2, 2, 0, bias=False),
+                         *[ResBlock(cout) for _ in range(nb)])
+
+
+class ResUNet(nn.Module):
+    """4-level residual U-Net denoiser (``models/ResUNet.py:7-42``)."""
+
+    def __init__(self, in_nc=1, out_nc=1, nc=(64, 128, 256, 512), nb=2):
+        super().__init__()
+        self.m_head = nn.Conv2d(in_nc, nc[0], 3, 1, 1, bias=False)
+        self.m_down1 = _down(nc[0], nc[1], nb)
+        self.m_down2 = _down(nc[1], nc[2], nb)
+        self.m_down3 = _down(nc[2], nc[3], nb)
+        self.m_body = nn.Sequential(*[ResBlock(nc[3]) for _ in range(nb)])
+        self.m_up3 = _up(nc[3], nc[2], nb)
+        self.m_up2 = _up(nc[2], nc[1], nb)
+        self.m_up1 = _up(nc[1], nc[0], nb)
+        self.m_tail = nn.Conv2d(nc[0], out_nc, 3, 1, 1, bias=False)
+
+    def forward(self, x):
+        h, w = x.shape[-2:]
+        pb, pr = (-h) % 8, (-w) % 8
+        if pb or pr:
+            x = F.pad(x, (0, pr, 0, pb), mode="replicate")
+        x1 = self.m_head(x)
+        x2 = self.m_down1(x1)
+        x3 = self.m_down2(x2)
+        x4 = self.m_down3(x3)
+        x = self.m_body(x4)
+        x = self.m_up3(x + x4)
+        x = self.m_up2(x + x3)
+        x = self.m_up1(x + x2)
+        x = self.m_tail(x + x1)
+        return x[..., :h, :w]
+
+
+class ZUpdateResUNet(nn.Module):
+    """Z step: ``z = ResUNet((x + u1).float())`` (runtime ``Z_Update_ResUNet`` at
+    ``models/Unrolled_ADMM.py:349-357``).  The attribute is ``net`` so keys read ``Z.net.*``."""
+
+    def __init__(self):
+        super().__init__()
+        self.net = ResUNet()
+
+    def forward(self, z):
+        return self.net(z.float())
+
+
+class _DoubleConv(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.double_conv = nn.Sequential(
+            nn.Conv2d(cin, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True),
+            nn.Conv2d(cout, cout, 3, padding=1), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+
+    def forward(self, x):
+        return self.double_conv(x)
+
+
+class _Down(nn.Module):
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.maxpool_conv = nn.Sequential(nn.MaxPool2d(2), _DoubleConv(cin, cout))
+
+    def forward(self, x):
+        return self.maxpool_conv(x)
+
+
+class SubNet(nn.Module):
+    """Per-galaxy ADMM penalty predictor (``models/Unrolled_ADMM.py:59-90``).
+
+    ``forward(kernel [N,1,h,w], alpha [N,1,1,1]) -> (rho1 [N,1,1,n], rho2 [N,1,1,n])``.
+    The PSF is zero-padded (or cropped, for h > 128) to 128x128 with floor/ceil split, exactly as
+    ``F.pad`` does at ``:79-81``; the |FFT|^2 feature runs through torch.fft (hipFFT on the GPU),
+    which is 1 small FFT per forward and is off the hot path.
+    """
+
+    def __init__(self, n):
+        super().__init__()
+        self.n = n
+        self.conv_layers = nn.Sequential(_Down(1, 4), _Down(4, 8), _Down(8, 16), _Down(16, 16))
+        self.mlp = nn.Sequential(nn.Linear(16 * 8 * 8 + 1, 64), nn.ReLU(inplace=True),
+                                 nn.Linear(64, 64), nn.ReLU(inplace=True),
+                                 nn.Linear(64, 2 * n), nn.Softplus())
+
+    def forward(self, kernel, alpha):
+        N, _, h, w = kernel.shape
+        h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
+        w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2
+        k_pad = F.pad(kernel, (w1, w2, h1, h2), "constant", 0)
+        Hk = torch.fft.fftn(k_pad, dim=[2, 3])
+        feat = self.conv_layers((torch.abs(Hk) ** 2).float())
+        feat = torch.cat((feat.view(N, 1, 16 * 8 * 8), alpha.float().view(N, 1, 1)), dim=2)
+        out = self.mlp(feat) + 1e-6
+        rho1 = out[:, :, 0:self.n].view(N, 1, 1, self.n)
+        rho2 = out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
+        return rho1, rho2
+
+
+def count_params(m):
+    return sum(p.numel() for p in m.parameters())
+
+
+__all__ = ["ResUNet", "ResBlock", "ZUpdateResUNet", "SubNet", "count_params"]

@@ -1,0 +1,3 @@
+"""Drop-in for reference ``models/Unrolled_ADMM.py`` (``Unrolled_ADMM`` :153-215, ``SubNet`` :59-90)."""
+from gdeconv.models import Unrolled_ADMM  # noqa: F401
+from gdeconv.nets import SubNet, ZUpdateResUNet as Z_Update_ResUNet  # noqa: F401

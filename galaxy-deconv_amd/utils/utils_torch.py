@@ -1,0 +1,3 @@
+"""Drop-in for reference ``utils/utils_torch.py`` hot-path helpers (``psf_to_otf`` :79-92,
+``conv_fft_batch`` :46-50, ``pad_double`` :11-13, ``crop_half`` :16-18) on the HIP engine."""
+from gdeconv.spectral import conv_fft_batch, crop_half, pad_double, psf_to_otf  # noqa: F401

@@ -1,0 +1,96 @@
+/* gdeconv.h - C ABI of the MI355X spectral deconvolution engine (libgdeconv.so, gfx950).
+ *
+ * Conventions (every entry point):
+ *   - plain C types only; images are fp32 [N][H][W] row-major (the NCHW C=1 tensors of the
+ *     reference), per-galaxy scalars are (pointer, stride-in-elements) pairs, stride 0 = broadcast;
+ *   - every pointer is a caller-allocated DEVICE pointer; the library never allocates, copies to
+ *     the host or synchronises: work is enqueued on `stream` (a hipStream_t, e.g. torch's current
+ *     stream) and the call returns immediately, so calls can be captured in a hipGraph;
+ *   - return GD_OK (0) or a negative GD_ERR_* code; gd_last_error() gives a per-thread message.
+ *     No C++ exception crosses the ABI.  Re-entrant across streams given distinct workspaces;
+ *   - spectra are half spectra stored TRANSPOSED, complex64 [N][W/2+1][H] (kx-major, ky
+ *     contiguous); `ws` is a workspace of gd_workspace_bytes(N, H, W) bytes;
+ *   - supported sizes: square H = W in {32, 48, 64, 96, 128, 256}; PSFs square, even side <= H.
+ *
+ * Reference interfaces replaced (paths relative to mbertagna/Galaxy-Deconv @ 2025-03-07):
+ *   gd_psf_to_otf       utils/utils_torch.py:79-92   psf_to_otf(ker, size)
+ *   gd_conv_fft_batch   utils/utils_torch.py:46-50   conv_fft_batch(H, x)   (conj=1: conv_fft_batch(conj(H), x))
+ *   gd_rfft2/gd_irfft2  utils/utils_torch.py:22-27   fftn / ifftn over dims [2,3] (real input, half spectrum)
+ *   gd_admm_init        models/Unrolled_ADMM.py:181-196 + init_l2 :170-175 (+ first V step of :207)
+ *   gd_admm_iter        models/Unrolled_ADMM.py:199-214 loop body around the denoiser call :208
+ *                       (X_Update :315-319, V_Update_{Poisson,Gaussian} :326-328/:335-336, duals
+ *                       :212-213, next V step, output scaling :215)
+ *   gd_wiener           models/Wiener.py:10-20       Wiener.forward(y, psf, alpha)
+ *   gd_richardson_lucy  models/Richard_Lucy.py:10-24 Richard_Lucy(n_iters).forward(y, psf)
+ */
+#ifndef GDECONV_H
+#define GDECONV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GD_ABI_VERSION 1
+
+#define GD_OK 0
+#define GD_ERR_ARG (-1)
+#define GD_ERR_UNSUPPORTED (-2)
+#define GD_ERR_HIP (-3)
+
+#define GD_LLH_GAUSSIAN 0
+#define GD_LLH_POISSON 1
+
+int gd_abi_version(void);
+const char* gd_last_error(void);
+int gd_supported_size(int H, int W);
+size_t gd_workspace_bytes(int N, int H, int W);
+size_t gd_otf_bytes(int N, int H, int W);
+
+/* OTF of h x w PSFs placed in an H x W image with pixel (h/2, w/2) circularly shifted to (0,0). */
+int gd_psf_to_otf(const float* psf, long long psf_gstride, int h, int w, int N, int H, int W,
+                  void* otf_half, void* ws, void* stream);
+
+/* out = Re IFFT2(FFT2(x) * H) (conj != 0: * conj(H)). */
+int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out, int N, int H, int W,
+                      void* ws, void* stream);
+
+/* Forward real 2D FFT into image slot 0 of a workspace-shaped buffer `spec`
+ * (gd_workspace_bytes(N,H,W) bytes; spectrum = first N*(W/2+1)*H complex of each galaxy's slot 0,
+ * i.e. element [g][0][kx][ky]).  gd_irfft2 inverts it in place (spec is clobbered). */
+int gd_rfft2(const float* x, void* spec, int N, int H, int W, void* stream);
+int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
+
+/* ADMM setup: OTF, x0 = clamp(init_l2), u1 = 0, u2 = 0, first V step.
+ * Outputs: otf_half, u1 (zeros), wv = v1 - u2 (= v1), zin = x0 (= x0 + u1, the first denoiser input).
+ * rho2 = the first iteration's rho2 (rho2_iters[..., 0]). */
+int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
+                 const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
+                 int llh, int N, int H, int W, void* otf_half, float* u1, float* wv, float* zin,
+                 void* ws, void* stream);
+
+/* One ADMM iteration after the denoiser produced z from zin:
+ *   X-update, u1 += x - z, u2 += conv(H,x) - v, then (unless last) the next V step with rho2_next
+ *   -> u1, wv = v_next - u2, zin_or_out = x + u1 (next denoiser input);
+ *   last != 0 -> zin_or_out = x (times alpha for Poisson), u1 / wv untouched.
+ * z may alias zin_or_out (identity denoiser). */
+int gd_admm_iter(const float* y, const void* otf_half, const float* z, float* u1, float* wv,
+                 float* zin_or_out, const float* alpha, long long alpha_stride, const float* rho1,
+                 long long rho1_stride, const float* rho2, long long rho2_stride,
+                 const float* rho2_next, long long rho2_next_stride, int llh, int last, int N, int H,
+                 int W, void* ws, void* stream);
+
+/* x = Re IFFT2(conj(H) FFT2(y) / (|H|^2 + 350/alpha)). */
+int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+              long long alpha_stride, float* x, int N, int H, int W, void* ws, void* stream);
+
+/* Richardson-Lucy from x0 = max(y,0); otf_half receives the OTF (gd_otf_bytes). */
+int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
+                       float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GDECONV_H */

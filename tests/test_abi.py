@@ -1,0 +1,66 @@
+"""The C-ABI library loads (no GPU needed) and exports exactly what include/gdeconv.h declares,
+with the ctypes binding's arity matching the header."""
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gdeconv.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(gd_\w+)\s*\(([^;]*?)\)\s*;", txt, flags=re.M | re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gdeconv import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("ge", os.path.join(ROOT, "__graft_entry__.py"))
+        ge = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(ge)
+        ge.build()
+    return _lib.load()
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("gd_psf_to_otf", "gd_conv_fft_batch", "gd_admm_init", "gd_admm_iter", "gd_wiener",
+                 "gd_richardson_lucy", "gd_rfft2", "gd_irfft2", "gd_last_error", "gd_workspace_bytes"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol(lib):
+    from gdeconv._lib import SIGNATURES
+    fns = header_functions()
+    assert set(fns) == set(SIGNATURES), "ctypes binding and header disagree"
+    for name, nargs in fns.items():
+        assert hasattr(lib, name), f"{name} not exported"
+        assert len(SIGNATURES[name][1]) == nargs, f"{name}: header has {nargs} args"
+
+
+def test_host_only_queries(lib):
+    assert lib.gd_abi_version() == 1
+    assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
+    assert lib.gd_supported_size(50, 50) == 0 and lib.gd_supported_size(256, 128) == 0
+    # workspace: N * 2 images * (W/2+1) * H complex64
+    assert lib.gd_workspace_bytes(4096, 256, 256) == 4096 * 2 * 129 * 256 * 8
+    assert lib.gd_otf_bytes(2, 48, 48) == 2 * 25 * 48 * 8
+
+
+def test_argument_errors_need_no_device(lib):
+    # validation happens before any HIP call: odd PSF, unsupported size, bad llh
+    assert lib.gd_psf_to_otf(None, 0, 5, 5, 1, 48, 48, None, None, None) == -1
+    assert b"even" in lib.gd_last_error()
+    assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 50, 50, None, None) == -2
+    assert lib.gd_admm_init(None, None, 0, 48, 48, None, 0, None, 0, 7, 1, 48, 48,
+                            None, None, None, None, None, None) == -1

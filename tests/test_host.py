@@ -1,0 +1,89 @@
+"""Host-side logic that needs no GPU: module trees / state_dict compatibility, deterministic
+weights, synthetic inputs, layout plumbing, argument validation."""
+import json
+import os
+
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def test_state_dict_keys_match_reference():
+    from gdeconv.models import Unrolled_ADMM
+    ref = json.load(open(os.path.join(GOLDEN, "state_dict_keys.json")))
+    sd = Unrolled_ADMM(n_iters=8, llh="Gaussian").state_dict()
+    assert [[k, list(v.shape)] for k, v in sd.items()] == ref
+    assert len(sd) == 98
+
+
+def test_subnet_false_parameters():
+    from gdeconv.models import Unrolled_ADMM
+    m = Unrolled_ADMM(n_iters=4, llh="Poisson", subnet=False)
+    sd = m.state_dict()
+    assert "rho1_iters" in sd and sd["rho2_iters"].shape == (4,)
+    assert not any(k.startswith("init.") for k in sd)
+
+
+def test_unsupported_variants_raise():
+    from gdeconv.models import Unrolled_ADMM
+    with pytest.raises(NotImplementedError):
+        Unrolled_ADMM(denoiser="XDenseUNet")
+    with pytest.raises(NotImplementedError):
+        Unrolled_ADMM(PnP=False)
+    with pytest.raises(ValueError):
+        Unrolled_ADMM(llh="Laplace")
+
+
+def test_weights_deterministic_and_loadable():
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.weights import make_state_dict
+    m = Unrolled_ADMM(n_iters=2, llh="Gaussian")
+    a, b = make_state_dict(m, 7), make_state_dict(m, 7)
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    c = make_state_dict(m, 8)
+    assert not torch.equal(a["Z.net.m_head.weight"], c["Z.net.m_head.weight"])
+    m.load_state_dict(a)
+
+
+def test_cpu_tensors_rejected_no_fallback():
+    from gdeconv.models import Unrolled_ADMM, Wiener
+    m = Unrolled_ADMM(n_iters=1, llh="Gaussian").eval()
+    y, k, a = torch.rand(1, 1, 48, 48), torch.rand(1, 1, 48, 48), torch.ones(1, 1, 1, 1)
+    with torch.no_grad(), pytest.raises(ValueError, match="ROCm"):
+        m(y, k, a)
+    with pytest.raises(ValueError, match="ROCm"):
+        Wiener()(y, k, a)
+
+
+def test_synth_batch_recipe():
+    from gdeconv.synth import make_batch
+    obs, psf, alpha, gt = make_batch(4, 48, seed=1)
+    assert obs.shape == (4, 1, 48, 48) and psf.shape == (4, 1, 48, 48) and alpha.shape == (4, 1, 1, 1)
+    assert torch.allclose(psf.sum((2, 3)), torch.full((4, 1), 1 / 16), rtol=1e-5)
+    assert torch.allclose(alpha.view(-1), obs.flatten(1).mean(1), rtol=1e-5)
+    o2, p2, a2, g2 = make_batch(4, 48, seed=1)
+    assert torch.equal(obs, o2) and torch.equal(psf, p2)
+    obs256, _, _, _ = make_batch(2, 256, seed=1)
+    assert obs256.shape == (2, 1, 256, 256)
+
+
+def test_half_full_layout_roundtrip():
+    """Plumbing between the reference's full OTF layout and the engine's half layout."""
+    from gdeconv.spectral import full_to_half, half_to_full
+    for L in (48, 64):
+        x = torch.rand(3, 1, L, L, dtype=torch.float64)
+        full = torch.fft.fftn(x, dim=[2, 3]).to(torch.complex64)
+        half = torch.fft.rfft2(x)[:, 0].transpose(1, 2).to(torch.complex64)
+        assert torch.allclose(full_to_half(full), half, atol=1e-4)
+        assert torch.allclose(half_to_full(half, L, L), full, atol=1e-4)
+
+
+def test_shard_range_covers_batch():
+    from gdeconv.dist import shard_range
+    for N in (1, 7, 4096, 32768):
+        for world in (1, 2, 3, 8):
+            parts = [shard_range(N, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == N
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1

@@ -1,0 +1,97 @@
+"""Pin the CPU oracle (oracle/admm_oracle.py) to golden vectors produced by the reference itself
+(tests/golden/make_golden.py imports /root/reference read-only).  fp32, CPU, bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import admm_oracle as O
+from conftest import golden
+
+WEIGHT_SEED = 1234  # tests/golden/make_golden.py
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+@pytest.mark.parametrize("tag", ["48", "256"])
+def test_psf_to_otf_and_conv(tag):
+    g = golden("otf_conv.npz")
+    obs, psf = T(g[f"obs{tag}"]), T(g[f"psf{tag}"])
+    kpad, H = O.psf_to_otf(psf, obs.size())
+    assert torch.equal(kpad, T(g[f"kpad{tag}"]))
+    half = torch.view_as_real(H[..., : obs.shape[-1] // 2 + 1].contiguous())
+    assert torch.equal(half, T(g[f"otf{tag}"]))
+    assert torch.equal(O.conv_fft_batch(H, obs), T(g[f"conv_H{tag}"]))
+    assert torch.equal(O.conv_fft_batch(torch.conj(H), obs), T(g[f"conv_Ht{tag}"]))
+
+
+def test_psf_to_otf_quadrant_shift_matches_roll():
+    g = golden("otf_conv.npz")
+    psf = T(g["psf48"])
+    kpad, _ = O.psf_to_otf(psf, (1, 1, 64, 64))
+    ref = torch.zeros(1, 1, 64, 64)
+    ref[..., :48, :48] = psf
+    assert torch.equal(kpad, torch.roll(ref, (-24, -24), (2, 3)))
+
+
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+def test_admm256_identity_denoiser(llh):
+    g = golden("admm256_id.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    out = O.admm_forward(obs, psf, alpha, T(g[f"{llh}_rho1"]), T(g[f"{llh}_rho2"]), llh)
+    assert torch.equal(out, T(g[f"{llh}_out"]))
+
+
+def _denoiser_and_subnet(n):
+    from gdeconv.nets import SubNet, ZUpdateResUNet
+    from gdeconv.weights import make_state_dict
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.Z = ZUpdateResUNet()
+            self.init = SubNet(n)
+
+    m = M()
+    m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    return m.eval()
+
+
+@pytest.mark.parametrize("llh,n", [("Gaussian", 2), ("Gaussian", 8), ("Poisson", 2), ("Poisson", 8)])
+def test_admm48_full_model(llh, n):
+    """Oracle + host-side ResUNet/SubNet mirrors reproduce the reference end to end."""
+    torch.set_num_threads(8)
+    g = golden("admm48.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    m = _denoiser_and_subnet(n)
+    with torch.no_grad():
+        rho1, rho2 = m.init(psf, alpha)
+        assert torch.equal(rho1, T(g[f"{llh}_n{n}_rho1"]))
+        assert torch.equal(rho2, T(g[f"{llh}_n{n}_rho2"]))
+        trace = {}
+        out = O.admm_forward(obs, psf, alpha, rho1, rho2, llh, denoise=m.Z, trace=trace)
+    assert torch.equal(out, T(g[f"{llh}_n{n}_out"]))
+    if f"{llh}_n{n}_v" in g:
+        for k in ("v", "z"):
+            assert torch.equal(torch.stack(trace[k]), T(g[f"{llh}_n{n}_{k}"]))
+        assert torch.equal(torch.stack(trace["x"][1:]), T(g[f"{llh}_n{n}_x"]))
+
+
+@pytest.mark.parametrize("tag", ["48", "256"])
+def test_wiener_and_richardson_lucy(tag):
+    torch.set_num_threads(8)
+    g = golden("wiener_rl.npz")
+    obs, psf, alpha = T(g[f"obs{tag}"]), T(g[f"psf{tag}"]), T(g[f"alpha{tag}"])
+    assert torch.equal(O.wiener(obs, psf, alpha), T(g[f"wiener{tag}"]))
+    assert torch.equal(O.richardson_lucy(obs, psf, 10), T(g[f"rl10_{tag}"]))
+    assert torch.equal(O.richardson_lucy(obs, psf, 100), T(g[f"rl100_{tag}"]))
+
+
+def test_fp64_restatement_close_to_fp32_reference():
+    """The fp32 reference itself sits within a few 1e-6 (normwise) of exact arithmetic; this is
+    the budget a different correct fp32 FFT (the HIP engine) has against the 1e-5 parity bar."""
+    g = golden("admm256_id.npz")
+    obs, psf, alpha = T(g["obs"]).double(), T(g["psf"]).double(), T(g["alpha"]).double()
+    out = O.admm_forward(obs, psf, alpha, T(g["Gaussian_rho1"]).double(), T(g["Gaussian_rho2"]).double())
+    assert float(O.normwise_error(T(g["Gaussian_out"]), out).max()) < 2e-6
