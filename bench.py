@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: unrolled PnP-ADMM spectral engine, galaxies/s at 256x256, n_iters=8 (BASELINE.json).
+
+One "step" = one forward of the drop-in ``Unrolled_ADMM(n_iters=8, llh='Gaussian')`` over this
+rank's batch (default 4096 galaxies of 256x256 fp32 = configs[2]; 8 ranks x 4096 = configs[3]):
+SubNet (PyTorch) -> OTF + init_l2 -> 8 x [X-update / duals / V step] on the HIP engine, with the
+denoiser replaced by the identity so the timed region is exactly the hot path the engine owns
+(the ResUNet stays PyTorch per the north star; its end-to-end cost is reported separately as
+``end_to_end`` on a sample).  Inputs are synthetic (``gdeconv.synth``), weights deterministic
+(``gdeconv.weights``), all resident in HBM before timing.
+
+  python bench.py [--gpus N --steps K --warmup W]        # N>1: launched by torch.distributed.run
+
+Rank 0 prints ONE JSON line (value = all ranks' galaxies / max-over-ranks wall time).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "galaxy-deconv_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured float4 copy)
+
+# kernel mode ids (gd_engine.hip enums) -> readable names
+MODE_NAMES = {
+    "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO"],
+    "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV"],
+    "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
+    "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
+}
+
+
+def pretty(name):
+    k, rest = name.split("<")
+    L, mode = rest.rstrip(">").split(",")
+    return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
+
+
+def kernel_bytes(name, L, last_frac=0.0):
+    """Algorithmic HBM bytes per galaxy for one launch of a kernel (each compulsory input read once,
+    each output written once; see DESIGN.md 'Kernels and their rooflines')."""
+    img = L * L * 4                  # one fp32 image
+    half = (L // 2 + 1) * L * 8      # one complex64 half spectrum
+    k = pretty(name)
+    table = {
+        f"k_row_fwd<{L},ITER>": 3 * img + 2 * half,          # z, u1, w -> T(2)
+        f"k_col<{L},ITER>": 5 * half,                        # T(2) + OTF -> T(2)
+        f"k_row_inv<{L},ITER>": 2 * half + 7 * img,          # T(2), z, u1, w, y -> u1, w, zin
+        f"k_row_fwd<{L},PSF_Y>": img + 2 * half,             # y (+ tiny psf) -> T(2)
+        f"k_col<{L},OTF_INIT>": 2 * half + 2 * half,         # T(2) -> OTF, T(1)
+        f"k_row_invfwd<{L},CLAMP>": 2 * half + img,          # T(1) -> zin, T(1)
+        f"k_col<{L},CONV>": 3 * half,                        # T(1) + OTF -> T(1)
+        f"k_row_inv<{L},INIT>": half + 4 * img,              # T(1), zin?, y -> u1, w
+    }
+    b = table.get(k)
+    if b is not None and k == f"k_row_inv<{L},ITER>" and last_frac:
+        b = b * (1 - last_frac) + (2 * half + img) * last_frac   # last iteration writes x only
+    return b
+
+
+def survey_bytes_per_galaxy(L, n, h=48):
+    """B = 4*HW*(4 + 16 n) + 4 h w (ADMM spectral engine, per galaxy)."""
+    return 4 * L * L * (4 + 16 * n) + 4 * h * h
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=4096, help="galaxies per GPU")
+    p.add_argument("--size", type=int, default=256)
+    p.add_argument("--n-iters", type=int, default=8)
+    p.add_argument("--llh", default="Gaussian")
+    p.add_argument("--cpu-sample", type=int, default=64, help="galaxies in the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--e2e-sample", type=int, default=64, help="galaxies for the ResUNet end-to-end sample")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
+    return p.parse_args()
+
+
+def build_model(n_iters, llh, dev, seed=1234):
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.weights import make_state_dict
+    m = Unrolled_ADMM(n_iters=n_iters, llh=llh)
+    m.load_state_dict(make_state_dict(m, seed))
+    return m.to(dev).eval()
+
+
+def cpu_baseline(args):
+    """The oracle (PyTorch CPU restatement of the reference) on a bounded sample of the same
+    workload: same model config, denoiser = identity, SubNet rhos from the same weights."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import admm_oracle as O
+    from gdeconv.synth import make_batch
+    n = args.cpu_sample
+    obs, psf, alpha, _ = make_batch(n, args.size, seed=777)
+    m = build_model(args.n_iters, args.llh, "cpu")
+    with torch.no_grad():
+        rho1, rho2 = m.init(psf, alpha)
+        t_total, done = 0.0, 0
+        O.admm_forward(obs[:2], psf[:2], alpha[:2], rho1[:2], rho2[:2], args.llh)  # warm
+        while t_total < args.cpu_seconds or done == 0:
+            t0 = time.perf_counter()
+            O.admm_forward(obs, psf, alpha, rho1, rho2, args.llh)
+            t_total += time.perf_counter() - t0
+            done += n
+    return {"value": done / t_total, "unit": "galaxies/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/admm_oracle.admm_forward (PyTorch CPU restatement of the reference), "
+                      f"{n} galaxies x {args.size}^2, n_iters={args.n_iters}, {args.llh}, denoiser=identity, "
+                      f"{done // n} passes, {t_total:.1f}s"}
+
+
+def main():
+    args = parse()
+    from gdeconv import _lib
+    from gdeconv.dist import init_process_group
+    from gdeconv.synth import make_batch
+
+    rank, world, local = init_process_group()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    _lib.load()
+
+    N, L, n = args.batch, args.size, args.n_iters
+    obs, psf, alpha, _ = make_batch(N, L, seed=20250307 + rank, device=dev)
+    model = build_model(n, args.llh, dev)
+    denoiser = model.Z
+    model.Z = torch.nn.Identity()            # spectral engine: the HIP hot path
+
+    def step():
+        return model(obs, psf, alpha)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        _lib.profile_enable(False)
+        kstats = _lib.profile_collect()
+        assert torch.isfinite(out).all(), "non-finite output"
+
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    gal_s = N * world * args.steps / elapsed
+
+    gather_ms = None
+    if world > 1:
+        from gdeconv.dist import gather_batch
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        gather_batch(out, N * world)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    # per-kernel live timing (HIP events on the engine's launch stream over the timed region)
+    kernels = {pretty(k): {"avg_ms": ms / c, "launches": c} for k, (ms, c) in kstats.items()}
+    dom_raw = max(kstats, key=lambda k: kstats[k][0])
+    dom_ms = kstats[dom_raw][0] / kstats[dom_raw][1]
+    last_frac = 1.0 / n if pretty(dom_raw) == f"k_row_inv<{L},ITER>" else 0.0
+    per_gal = kernel_bytes(dom_raw, L, last_frac)
+    achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        ent = tj.get("kernels", {}).get(pretty(dom_raw))
+        if ent and tj.get("batch") == N and tj.get("size") == L:
+            traffic = ent.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "hbm", "kernel": pretty(dom_raw), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic, "algorithmic_bytes_per_launch": per_gal * N if per_gal else None,
+                "avg_launch_ms": dom_ms}
+    engine_gbs = survey_bytes_per_galaxy(L, n) * gal_s / world / 1e9
+
+    rec = {
+        "metric": f"galaxies/sec ({L}x{L}, n_iters={n}) - unrolled ADMM spectral engine",
+        "value": gal_s, "unit": "galaxies/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (gdeconv.synth, seeded); deterministic random weights (gdeconv.weights)",
+        "config": {"workload": f"Unrolled_ADMM(n_iters={n}, llh='{args.llh}') forward, denoiser=identity "
+                               f"(spectral engine: SubNet + OTF + init_l2 + {n} ADMM iterations), "
+                               f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])",
+                   "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
+                   "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)"},
+        "roofline": roofline,
+        "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
+                       "frac_of_peak": engine_gbs / HBM_PEAK_GBS},
+        "kernels": kernels,
+    }
+    if gather_ms is not None:
+        rec["gather_ms"] = gather_ms
+
+    if rank == 0 and world == 1 and not args.no_e2e:
+        model.Z = denoiser
+        G = min(args.e2e_sample, N)
+        o2, p2, a2 = obs[:G].contiguous(), psf[:G].contiguous(), alpha[:G].contiguous()
+        with torch.no_grad():
+            model(o2, p2, a2)
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            model(o2, p2, a2)
+            torch.cuda.synchronize()
+            te = time.perf_counter() - te
+        rec["end_to_end"] = {"value": G / te, "unit": "galaxies/s",
+                             "sample": f"{G} galaxies, full model with PyTorch ResUNet (fp32, MIOpen), 1 timed forward"}
+        del o2, p2, a2
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,18 +1,19 @@
 // galaxy-deconv_amd: MI355X-native spectral engine for unrolled PnP-ADMM deconvolution.
 //
 // Three streaming kernels per 2D spectral round trip, all fp32:
-//   k_row_fwd  (RF)  : per block RW rows of one galaxy.  Two real images p, w are packed as one
-//                      complex line c = p + i w, length-L FFT along the row inside one wave, split
-//                      into the two half spectra (kx = 0..L/2), stored TRANSPOSED to the
-//                      workspace T[N][2][K][L] (K = L/2+1) so the column pass reads contiguous
-//                      columns.  Mode-specific producers fuse the preceding elementwise work
-//                      (z - u1, PSF placement + circular shift, max(y,0)/alpha, ...).
-//   k_col      (C)  : per line one (galaxy, kx) column of both images: column FFTs, the fused
+//   k_row_fwd  (RF)  : per block RB rows of one galaxy (of one or two images).  Two adjacent rows
+//                      of the same image are packed as one complex line (even row = Re, odd = Im),
+//                      length-L FFT along the row inside one wave, split into the two rows' half
+//                      spectra (kx = 0..L/2) and stored TRANSPOSED to the workspace
+//                      T[N][2][K][L] (K = L/2+1) so the column pass reads contiguous columns.
+//                      Mode-specific producers fuse the preceding elementwise work (z - u1, PSF
+//                      placement + circular shift, max(y,0)/alpha, ...).
+//   k_col      (C)  : per line one (galaxy, kx) column of each image: column FFTs, the fused
 //                      spectral operator (X-update divide, Wiener divide, OTF capture, conv
 //                      multiply), inverse column FFTs, stored back in place.
-//   k_row_inv  (RI) : per block RW rows: Hermitian extension of the two half spectra packed as
-//                      R + iS, inverse row FFT (Re = r, Im = s), and the fused elementwise sink
-//                      (dual updates, V step, next-iteration denoiser input, outputs).
+//   k_row_inv  (RI) : per block RB rows: Hermitian extension of row-pair half spectra, inverse row
+//                      FFT, result image staged in LDS, then the fused elementwise sink with
+//                      16-byte coalesced accesses (dual updates, V step, next denoiser input, output).
 //   k_row_invfwd (RIF): RI + a pointwise nonlinearity + RF of the result in one kernel (clamp in
 //                      init_l2, Richardson-Lucy ratio / multiplicative update).
 //
@@ -32,7 +33,10 @@
 
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/gdeconv.h"
 #include "gd_fft.hpp"
@@ -72,22 +76,23 @@ enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
 constexpr int rows_per_block(int lpb, int L) {
     int rw = lpb < L ? lpb : L;
-    while (L % rw) --rw;
+    while (L % rw || rw % 2) --rw;
     return rw;
 }
+constexpr int cmax(int x, int y) { return x > y ? x : y; }
 
 template <int L>
 struct Geo {
     static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2;
     static constexpr int K = L / 2 + 1;
     static constexpr int LPB = 256 / F1;               // lines per 256-thread block
-    static constexpr int RW = rows_per_block(LPB, L);  // rows per row-kernel block (divides L)
-    static constexpr int ROW_THREADS = RW * F1;
+    static constexpr int RB = rows_per_block(LPB, L);  // rows per row-kernel block (even, divides L)
     static constexpr int RLD = L + 2;                  // row buffer leading dim (bank spread)
     static constexpr int XCH = xch_elems<L>();
-    static constexpr int ROW_LDS = (RW * RLD > LPB * XCH) ? RW * RLD : LPB * XCH;
+    // row kernels (worst case two images = RB lines): row buffer | exchange areas | result image
+    static constexpr int ROW_LDS = cmax(cmax(RB * RLD, RB * XCH), RB * L);
     static constexpr int COL_LDS = LPB * XCH;
-    static_assert(L % RW == 0, "rows per block must divide L");
+    static_assert(L % RB == 0 && RB % 2 == 0, "rows per block must be even and divide L");
 };
 
 __device__ __forceinline__ size_t tidx(int g, int img, int k, int row, int K, int L) {
@@ -113,87 +118,112 @@ __device__ __forceinline__ float v_step(int llh, float vt, float yp, float rho2,
 }
 
 // ---------------------------------------------------------------- row-side building blocks
-// Split packed row spectra C = FFT(p + i w) held in the row buffer into P and W half spectra
-// and store them transposed: T[g][img][k][row].
-template <int L, bool TWO>
-__device__ __forceinline__ void split_store(const Args& a, const float2* rowbuf, int g, int row0,
-                                            int tid, int nthreads) {
+// Row kernels pack two ADJACENT ROWS OF THE SAME IMAGE into one complex line (row 2m -> real part,
+// row 2m+1 -> imaginary part).  Packing two different images instead would extract the smaller
+// one's spectrum from the rounding noise of the larger (a PSF of sum 1/16 next to an observation of
+// ~1e2 ADU loses every digit), while rows of one image share its scale exactly as a 2D FFT does.
+template <int L, int NI>
+struct RowGeo {
     using G = Geo<L>;
-    for (int idx = tid; idx < G::K * G::RW; idx += nthreads) {
-        const int k = idx / G::RW, rr = idx - k * G::RW;
-        const float2 C = rowbuf[rr * G::RLD + k];
-        const float2 D = rowbuf[rr * G::RLD + (k == 0 ? 0 : L - k)];
-        // P = (C + conj D)/2 ; W = (C - conj D)/(2i)
-        a.T[tidx(g, 0, k, row0 + rr, G::K, L)] = make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));
-        if (TWO) a.T[tidx(g, 1, k, row0 + rr, G::K, L)] = make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+    static constexpr int RB = G::RB;        // rows per block, per image (even, divides L)
+    static constexpr int PAIRS = RB / 2;    // lines per image
+    static constexpr int LINES = NI * PAIRS;
+    static constexpr int THREADS = LINES * G::F1;
+    static_assert(RB % 2 == 0, "row pairs");
+};
+
+// Split line spectra C = FFT(row_even + i row_odd) (row buffer [line][k]) into the two rows'
+// half spectra, stored transposed T[g][im][k][row0 + rr]; consecutive threads take consecutive rows.
+template <int L, int NI>
+__device__ __forceinline__ void split_store(const Args& a, const float2* rowbuf, int g, int row0, int tid) {
+    using G = Geo<L>;
+    using R = RowGeo<L, NI>;
+    for (int idx = tid; idx < NI * G::K * R::RB; idx += R::THREADS) {
+        const int rr = idx % R::RB, t = idx / R::RB;
+        const int k = t % G::K, im = t / G::K;
+        const int line = im * R::PAIRS + (rr >> 1);
+        const float2 C = rowbuf[line * G::RLD + k];
+        const float2 D = rowbuf[line * G::RLD + (k == 0 ? 0 : L - k)];
+        const float2 o = (rr & 1) ? make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x))   // (C - conj D)/(2i)
+                                  : make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));  // (C + conj D)/2
+        a.T[tidx(g, im, k, row0 + rr, G::K, L)] = o;
     }
 }
 
-// Load the two half spectra of rows [row0, row0+RW) and build the Hermitian-extended packed
-// spectrum D = R + i S over kx in [0, L) in the row buffer.
-template <int L, bool TWO>
-__device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g, int row0, int tid,
-                                            int nthreads) {
+// Gather the half spectra of rows 2m, 2m+1 of each image into the Hermitian-extended packed line
+// spectrum D = R_even + i R_odd over kx in [0, L) (row buffer [line][k]).  One 16-byte load per
+// (image, k, pair): the two rows are adjacent in the transposed layout.
+template <int L, int NI>
+__device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g, int row0, int tid) {
     using G = Geo<L>;
-    for (int idx = tid; idx < G::K * G::RW; idx += nthreads) {
-        const int k = idx / G::RW, rr = idx - k * G::RW;
-        float2 R = a.T[tidx(g, 0, k, row0 + rr, G::K, L)];
-        float2 S = TWO ? a.T[tidx(g, 1, k, row0 + rr, G::K, L)] : make_float2(0.f, 0.f);
-        const bool self = (k == 0) || (2 * k == L);  // self-conjugate bins: keep real parts only
+    using R = RowGeo<L, NI>;
+    for (int idx = tid; idx < NI * G::K * R::PAIRS; idx += R::THREADS) {
+        const int m = idx % R::PAIRS, t = idx / R::PAIRS;
+        const int k = t % G::K, im = t / G::K;
+        const float4 q = *reinterpret_cast<const float4*>(a.T + tidx(g, im, k, row0 + 2 * m, G::K, L));
+        float2 Re = make_float2(q.x, q.y), Ro = make_float2(q.z, q.w);
+        const bool self = (k == 0) || (2 * k == L);  // self-conjugate bins: real parts only (irfft)
         if (self) {
-            R.y = 0.f;
-            S.y = 0.f;
+            Re.y = 0.f;
+            Ro.y = 0.f;
         }
-        rowbuf[rr * G::RLD + k] = make_float2(R.x - S.y, R.y + S.x);
-        if (!self) rowbuf[rr * G::RLD + (L - k)] = make_float2(R.x + S.y, S.x - R.y);
+        const int line = im * R::PAIRS + m;
+        rowbuf[line * G::RLD + k] = make_float2(Re.x - Ro.y, Re.y + Ro.x);
+        if (!self) rowbuf[line * G::RLD + (L - k)] = make_float2(Re.x + Ro.y, Ro.x - Re.y);
     }
 }
 
 // ---------------------------------------------------------------- RF: row forward
+template <int MODE>
+struct RfTraits {
+    static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE) ? 1 : 2;
+};
+
+// Value of image `im` at pixel (r, c) for the RF producers.
 template <int L, int MODE>
-__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_fwd(Args a) {
+__device__ __forceinline__ float rf_source(const Args& a, int g, int im, int r, int c) {
+    const size_t pix = ((size_t)g * L + r) * L + c;
+    if constexpr (MODE == RF_ITER) {
+        return im == 0 ? a.a0[pix] - a.a1[pix] : a.a2[pix];          // z - u1 | v - u2
+    } else if constexpr (MODE == RF_PSF_Y) {
+        return im == 0 ? shifted_psf(a, g, r, c, L) : fmaxf(a.y[pix], 0.f) / a.alpha(g);
+    } else if constexpr (MODE == RF_PSF_YP) {
+        if (im == 0) return shifted_psf(a, g, r, c, L);
+        const float yp = fmaxf(a.y[pix], 0.f);
+        a.o0[pix] = yp;                                                // Richardson-Lucy x0
+        return yp;
+    } else if constexpr (MODE == RF_PSF_RAW) {
+        return im == 0 ? shifted_psf(a, g, r, c, L) : a.y[pix];
+    } else if constexpr (MODE == RF_PSF) {
+        return shifted_psf(a, g, r, c, L);
+    } else if constexpr (MODE == RF_ONE) {
+        return a.a0[pix];
+    } else {
+        return im == 0 ? a.a0[pix] : a.a1[pix];
+    }
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI>::THREADS)) void k_row_fwd(Args a) {
+    constexpr int NI = RfTraits<MODE>::NI;
     using G = Geo<L>;
+    using R = RowGeo<L, NI>;
     constexpr int F1 = G::F1, F2 = G::F2;
-    constexpr bool TWO = (MODE != RF_PSF && MODE != RF_ONE);
     __shared__ float2 tw[L];
     __shared__ float2 lds[G::ROW_LDS];
     const int tid = threadIdx.x;
-    const int blocks_per_g = L / G::RW;
+    const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
-    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * R::RB;
     const int line = tid / F1, j = tid - line * F1;
-    const int r = row0 + line;
-    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
-
-    const size_t rbase = ((size_t)g * L + r) * L;
+    const int im = line / R::PAIRS, m = line - im * R::PAIRS;
+    const int rA = row0 + 2 * m;
+    fill_twiddles<L>(tw, tid, R::THREADS);
     float2 v[F2];
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int c = j + F1 * s;
-        const size_t pix = rbase + c;
-        float p = 0.f, w = 0.f;
-        if constexpr (MODE == RF_ITER) {
-            p = a.a0[pix] - a.a1[pix];  // z - u1
-            w = a.a2[pix];              // v - u2
-        } else if constexpr (MODE == RF_PSF_Y) {
-            p = shifted_psf(a, g, r, c, L);
-            w = fmaxf(a.y[pix], 0.f) / a.alpha(g);
-        } else if constexpr (MODE == RF_PSF_YP) {
-            p = shifted_psf(a, g, r, c, L);
-            w = fmaxf(a.y[pix], 0.f);
-            a.o0[pix] = w;  // Richardson-Lucy x0 = max(y, 0)
-        } else if constexpr (MODE == RF_PSF_RAW) {
-            p = shifted_psf(a, g, r, c, L);
-            w = a.y[pix];
-        } else if constexpr (MODE == RF_PSF) {
-            p = shifted_psf(a, g, r, c, L);
-        } else if constexpr (MODE == RF_ONE) {
-            p = a.a0[pix];
-        } else {
-            p = a.a0[pix];
-            w = a.a1[pix];
-        }
-        v[s] = make_float2(p, w);
+        v[s] = make_float2(rf_source<L, MODE>(a, g, im, rA, c), rf_source<L, MODE>(a, g, im, rA + 1, c));
     }
     __syncthreads();  // twiddles
     line_fft<L, false>(v, j, lds + line * G::XCH, tw);
@@ -201,7 +231,7 @@ __global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_fwd(Args a) {
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
-    split_store<L, TWO>(a, lds, g, row0, tid, G::ROW_THREADS);
+    split_store<L, NI>(a, lds, g, row0, tid);
 }
 
 // ---------------------------------------------------------------- C: column pass
@@ -314,122 +344,168 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 // ---------------------------------------------------------------- RI: row inverse + sink
 template <int MODE>
 struct RiTraits {
-    static constexpr bool TWO = (MODE == RI_ITER || MODE == RI_OUT2);
+    static constexpr int NI = (MODE == RI_ITER || MODE == RI_OUT2) ? 2 : 1;
 };
 
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int i, float x) {
+    if (i == 0) v.x = x; else if (i == 1) v.y = x; else if (i == 2) v.z = x; else v.w = x;
+}
+
 template <int L, int MODE>
-__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_inv(Args a) {
+__global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI>::THREADS)) void k_row_inv(Args a) {
+    constexpr int NI = RiTraits<MODE>::NI;
     using G = Geo<L>;
+    using R = RowGeo<L, NI>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
     const int tid = threadIdx.x;
-    const int blocks_per_g = L / G::RW;
+    const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
-    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * R::RB;
     const int line = tid / F1, j = tid - line * F1;
-    const int r = row0 + line;
-    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
-    gather_rows<L, RiTraits<MODE>::TWO>(a, lds, g, row0, tid, G::ROW_THREADS);
+    const int im = line / R::PAIRS, m = line - im * R::PAIRS;
+    fill_twiddles<L>(tw, tid, R::THREADS);
+    gather_rows<L, NI>(a, lds, g, row0, tid);
     __syncthreads();
     float2 v[F2];
 #pragma unroll
     for (int s = 0; s < F2; ++s) v[s] = lds[line * G::RLD + j + F1 * s];
     __syncthreads();  // row buffer -> exchange area
     line_fft<L, true>(v, j, lds + line * G::XCH, tw);
+    __syncthreads();  // every line done with its exchange area -> result image
+    float* res = reinterpret_cast<float*>(lds);  // [im][rr][c], RB x L per image
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int c = j + F1 * s;
+        res[(im * R::RB + 2 * m) * L + c] = v[s].x;
+        res[(im * R::RB + 2 * m + 1) * L + c] = v[s].y;
+    }
+    __syncthreads();
 
-    const size_t rbase = ((size_t)g * L + r) * L;
     float al = 1.f, r2n = 1.f, div = 1.f;
     if constexpr (MODE == RI_ITER || MODE == RI_INIT) {
         al = a.alpha(g);
         if (!(MODE == RI_ITER && a.last)) r2n = a.rho2n(g);
     }
     if constexpr (MODE == RI_RL_FINAL) div = a.otf[(size_t)g * G::K * L].x;  // conv(Ht, ones) = H(0,0)
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const size_t pix = rbase + j + F1 * s;
-        const float re = v[s].x, im = v[s].y;
+    const bool poisson = a.llh == GD_LLH_POISSON;
+    // elementwise sink over this block's RB x L pixels, 4 consecutive pixels per thread step
+    for (int q = tid * 4; q < R::RB * L; q += R::THREADS * 4) {
+        const int rr = q / L, c = q - rr * L;
+        const size_t pix = ((size_t)g * L + row0 + rr) * L + c;
+        const float4 X = ld4(res + rr * L + c);
         if constexpr (MODE == RI_ITER) {
-            // models/Unrolled_ADMM.py:207-213 (x = re, conv(H,x) = im)
-            const float z = a.a0[pix];
-            const float u1 = (a.o0[pix] + re) - z;     // u1 + x - z
-            const float u2 = im - a.o1[pix];           // u2 + Hx - v  (w = v - u2)
+            // models/Unrolled_ADMM.py:207-215 (x = image 0, conv(H, x) = image 1)
+            const float4 HX = ld4(res + (R::RB + rr) * L + c);
             if (a.last) {
-                a.o2[pix] = (a.llh == GD_LLH_POISSON) ? re * al : re;
+                float4 o = X;
+                if (poisson) o = make_float4(X.x * al, X.y * al, X.z * al, X.w * al);
+                st4(a.o2 + pix, o);
             } else {
-                const float yp = fmaxf(a.y[pix], 0.f);
-                const float vn = v_step(a.llh, im + u2, yp, r2n, al);
-                a.o0[pix] = u1;
-                a.o1[pix] = vn - u2;
-                a.o2[pix] = re + u1;                   // next denoiser input x + u1
+                const float4 Z = ld4(a.a0 + pix), U1 = ld4(a.o0 + pix), Wv = ld4(a.o1 + pix), Y = ld4(a.y + pix);
+                float4 u1o, wo, zo;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = f4(X, e), hx = f4(HX, e);
+                    const float u1 = (f4(U1, e) + x) - f4(Z, e);      // u1 + x - z
+                    const float u2 = hx - f4(Wv, e);                  // u2 + conv(H,x) - v  (w = v - u2)
+                    const float vn = v_step(a.llh, hx + u2, fmaxf(f4(Y, e), 0.f), r2n, al);
+                    f4set(u1o, e, u1);
+                    f4set(wo, e, vn - u2);
+                    f4set(zo, e, x + u1);                             // next denoiser input
+                }
+                st4(a.o0 + pix, u1o);
+                st4(a.o1 + pix, wo);
+                st4(a.o2 + pix, zo);
             }
         } else if constexpr (MODE == RI_INIT) {
-            // first V step with x = x0 (zin), u1 = u2 = 0: v = V(conv(H,x0) + 0, ...)
-            const float yp = fmaxf(a.y[pix], 0.f);
-            a.o1[pix] = v_step(a.llh, re + 0.0f, yp, r2n, al);
-            a.o0[pix] = 0.f;
+            // first V step with x = x0, u1 = u2 = 0: v = V(conv(H, x0) + 0, ...)
+            const float4 Y = ld4(a.y + pix);
+            float4 wo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f4set(wo, e, v_step(a.llh, f4(X, e) + 0.0f, fmaxf(f4(Y, e), 0.f), r2n, al));
+            st4(a.o1 + pix, wo);
+            st4(a.o0 + pix, make_float4(0.f, 0.f, 0.f, 0.f));
         } else if constexpr (MODE == RI_OUT1) {
-            a.o0[pix] = re;
+            st4(a.o0 + pix, X);
         } else if constexpr (MODE == RI_OUT2) {
-            a.o0[pix] = re;
-            a.o1[pix] = im;
+            st4(a.o0 + pix, X);
+            st4(a.o1 + pix, ld4(res + (R::RB + rr) * L + c));
         } else if constexpr (MODE == RI_RL_FINAL) {
-            a.o0[pix] = a.o0[pix] * re / div;          // x * numerator / divisor
+            const float4 X0 = ld4(a.o0 + pix);
+            float4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f4set(o, e, f4(X0, e) * f4(X, e) / div);   // x * numerator / divisor
+            st4(a.o0 + pix, o);
         }
     }
 }
 
 // ---------------------------------------------------------------- RIF: row inverse -> pointwise -> row forward
 template <int L, int MODE>
-__global__ __launch_bounds__(Geo<L>::ROW_THREADS) void k_row_invfwd(Args a) {
+__device__ __forceinline__ float rif_point(const Args& a, int g, int r, int c, float re, float div) {
+    const size_t pix = ((size_t)g * L + r) * L + c;
+    if constexpr (MODE == RIF_CLAMP) {
+        const float p = fminf(fmaxf(re, 0.f), 1.f);   // torch.clamp(x0, 0, 1)
+        a.o0[pix] = p;
+        return p;
+    } else if constexpr (MODE == RIF_RL_RATIO) {
+        return fmaxf(a.y[pix], 0.f) / re;             // y / Hx
+    } else {
+        const float p = a.o0[pix] * re / div;         // x * numerator / divisor
+        a.o0[pix] = p;
+        return p;
+    }
+}
+
+template <int L, int MODE>
+__global__ __launch_bounds__((RowGeo<L, 1>::THREADS)) void k_row_invfwd(Args a) {
     using G = Geo<L>;
+    using R = RowGeo<L, 1>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
     const int tid = threadIdx.x;
-    const int blocks_per_g = L / G::RW;
+    const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
-    const int row0 = (blockIdx.x - g * blocks_per_g) * G::RW;
+    const int row0 = (blockIdx.x - g * blocks_per_g) * R::RB;
     const int line = tid / F1, j = tid - line * F1;
-    const int r = row0 + line;
-    fill_twiddles<L>(tw, tid, G::ROW_THREADS);
-    gather_rows<L, false>(a, lds, g, row0, tid, G::ROW_THREADS);
+    const int rA = row0 + 2 * line;
+    fill_twiddles<L>(tw, tid, R::THREADS);
+    gather_rows<L, 1>(a, lds, g, row0, tid);
     __syncthreads();
     float2 v[F2];
 #pragma unroll
     for (int s = 0; s < F2; ++s) v[s] = lds[line * G::RLD + j + F1 * s];
     __syncthreads();
     line_fft<L, true>(v, j, lds + line * G::XCH, tw);
-
-    const size_t rbase = ((size_t)g * L + r) * L;
     float div = 1.f;
     if constexpr (MODE == RIF_RL_UPDATE) div = a.otf[(size_t)g * G::K * L].x;
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
-        const size_t pix = rbase + j + F1 * s;
-        const float re = v[s].x;
-        float p;
-        if constexpr (MODE == RIF_CLAMP) {
-            p = fminf(fmaxf(re, 0.f), 1.f);            // torch.clamp(x0, 0, 1)
-            a.o0[pix] = p;
-        } else if constexpr (MODE == RIF_RL_RATIO) {
-            p = fmaxf(a.y[pix], 0.f) / re;             // y / Hx
-        } else {
-            p = a.o0[pix] * re / div;                  // x * numerator / divisor
-            a.o0[pix] = p;
-        }
-        v[s] = make_float2(p, 0.f);
+        const int c = j + F1 * s;
+        v[s] = make_float2(rif_point<L, MODE>(a, g, rA, c, v[s].x, div),
+                           rif_point<L, MODE>(a, g, rA + 1, c, v[s].y, div));
     }
     line_fft<L, false>(v, j, lds + line * G::XCH, tw);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
-    split_store<L, false>(a, lds, g, row0, tid, G::ROW_THREADS);
+    split_store<L, 1>(a, lds, g, row0, tid);
 }
 
 // ---------------------------------------------------------------- host-side launch helpers
 thread_local std::string g_last_error;
+
+constexpr const char* kRowFwdName = "k_row_fwd";
+constexpr const char* kColName = "k_col";
+constexpr const char* kRowInvName = "k_row_inv";
+constexpr const char* kRowInvFwdName = "k_row_invfwd";
 
 inline int fail(int code, const char* msg) {
     g_last_error = msg;
@@ -445,30 +521,86 @@ inline int check_launch(const char* what) {
     return GD_OK;
 }
 
+// Opt-in per-kernel timing (gd_profile_*): every launch is bracketed by two hipEvents recorded on
+// the launch stream; durations are harvested by gd_profile_collect().  Off by default (no events,
+// graph-capturable).
+struct ProfEntry {
+    std::string name;
+    hipEvent_t start, stop;
+};
+struct ProfStat {
+    double ms = 0.0;
+    long long launches = 0;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfEntry> g_prof_pending;
+std::vector<hipEvent_t> g_prof_pool;
+std::map<std::string, ProfStat> g_prof_stats;
+
+inline hipEvent_t prof_event() {
+    if (!g_prof_pool.empty()) {
+        hipEvent_t e = g_prof_pool.back();
+        g_prof_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct ProfScope {
+    bool on;
+    ProfEntry ent;
+    hipStream_t st;
+    ProfScope(const std::string& name, hipStream_t s) : on(false), st(s) {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (!g_prof_on) return;
+        on = true;
+        ent.name = name;
+        ent.start = prof_event();
+        ent.stop = prof_event();
+        (void)hipEventRecord(ent.start, st);
+    }
+    ~ProfScope() {
+        if (!on) return;
+        (void)hipEventRecord(ent.stop, st);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof_pending.push_back(ent);
+    }
+};
+
 template <int L>
 struct Launcher {
     using G = Geo<L>;
-    static int row_grid(int N) { return N * (L / G::RW); }
+    static int row_grid(int N) { return N * (L / G::RB); }
     static int col_grid(int N) { return (N * G::K + G::LPB - 1) / G::LPB; }
+    static std::string nm(const char* k, int mode) {
+        return std::string(k) + "<" + std::to_string(L) + "," + std::to_string(mode) + ">";
+    }
 
     template <int MODE>
     static int rf(const Args& a, hipStream_t st) {
-        hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        ProfScope ps(nm(kRowFwdName, MODE), st);
+        hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, RfTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_fwd");
     }
     template <int MODE>
     static int col(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kColName, MODE), st);
         hipLaunchKernelGGL((k_col<L, MODE>), dim3(col_grid(a.N)), dim3(256), 0, st, a);
         return check_launch("k_col");
     }
     template <int MODE>
     static int ri(const Args& a, hipStream_t st) {
-        hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        ProfScope ps(nm(kRowInvName, MODE), st);
+        hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, RiTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_inv");
     }
     template <int MODE>
     static int rif(const Args& a, hipStream_t st) {
-        hipLaunchKernelGGL((k_row_invfwd<L, MODE>), dim3(row_grid(a.N)), dim3(G::ROW_THREADS), 0, st, a);
+        ProfScope ps(nm(kRowInvFwdName, MODE), st);
+        hipLaunchKernelGGL((k_row_invfwd<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, 1>::THREADS), 0, st, a);
         return check_launch("k_row_invfwd");
     }
 };
@@ -708,6 +840,48 @@ int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, 
     a.otf = reinterpret_cast<float2*>(otf_half);
     a.o0 = x;
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
+}
+
+int gd_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return GD_OK;
+}
+
+int gd_profile_collect(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto& e : g_prof_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(e.stop) != hipSuccess || hipEventElapsedTime(&ms, e.start, e.stop) != hipSuccess)
+            return fail(GD_ERR_HIP, "profile event query failed");
+        ProfStat& st = g_prof_stats[e.name];
+        st.ms += ms;
+        st.launches += 1;
+        g_prof_pool.push_back(e.start);
+        g_prof_pool.push_back(e.stop);
+    }
+    g_prof_pending.clear();
+    return (int)g_prof_stats.size();
+}
+
+int gd_profile_get(int i, char* name, int name_len, double* total_ms, long long* launches) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (i < 0 || i >= (int)g_prof_stats.size()) return fail(GD_ERR_ARG, "profile index out of range");
+    auto it = g_prof_stats.begin();
+    std::advance(it, i);
+    if (name && name_len > 0) {
+        std::strncpy(name, it->first.c_str(), (size_t)name_len - 1);
+        name[name_len - 1] = 0;
+    }
+    if (total_ms) *total_ms = it->second.ms;
+    if (launches) *launches = it->second.launches;
+    return GD_OK;
+}
+
+int gd_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_stats.clear();
+    return GD_OK;
 }
 
 }  // extern "C"

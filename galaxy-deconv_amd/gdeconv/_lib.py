@@ -36,6 +36,10 @@ SIGNATURES = {
                           _P, _P]),
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
+    "gd_profile_enable": (_I, [_I]),
+    "gd_profile_collect": (_I, []),
+    "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),
+    "gd_profile_reset": (_I, []),
 }
 
 _lib = None
@@ -62,6 +66,29 @@ def load(path=LIB_PATH):
         raise EngineError("libgdeconv.so ABI version mismatch")
     _lib = lib
     return lib
+
+
+def profile_enable(on=True):
+    load().gd_profile_enable(int(bool(on)))
+
+
+def profile_reset():
+    load().gd_profile_reset()
+
+
+def profile_collect():
+    """{kernel name: (total_ms, launches)} accumulated since the last reset (synchronises)."""
+    lib = load()
+    n = lib.gd_profile_collect()
+    if n < 0:
+        check(n, "gd_profile_collect")
+    out = {}
+    buf = ctypes.create_string_buffer(128)
+    for i in range(n):
+        ms, cnt = ctypes.c_double(), _LL()
+        check(lib.gd_profile_get(i, buf, 128, ctypes.byref(ms), ctypes.byref(cnt)), "gd_profile_get")
+        out[buf.value.decode()] = (ms.value, cnt.value)
+    return out
 
 
 def check(rc, what):

@@ -56,7 +56,10 @@ _WS = {}
 
 def workspace(N, H, W, device):
     """Per-device cached workspace of gd_workspace_bytes(N, H, W) bytes (grown on demand)."""
-    nbytes = int(_lib.load().gd_workspace_bytes(N, H, W))
+    lib = _lib.load()
+    if not lib.gd_supported_size(H, W):
+        raise ValueError(f"unsupported image size {H}x{W} (supported: square 32,48,64,96,128,256)")
+    nbytes = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
     if nbytes == 0:
         raise ValueError(f"unsupported image size {H}x{W} (supported: square 32,48,64,96,128,256)")
     key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()

@@ -89,6 +89,14 @@ int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, in
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
 
+/* Opt-in per-kernel timing: when enabled, every kernel launch is bracketed by hipEvents on its
+ * stream.  gd_profile_collect() waits for them and returns the number of distinct kernels;
+ * gd_profile_get(i, ...) reads the i-th (name, total ms, launches); gd_profile_reset() clears. */
+int gd_profile_enable(int on);
+int gd_profile_collect(void);
+int gd_profile_get(int i, char* name, int name_len, double* total_ms, long long* launches);
+int gd_profile_reset(void);
+
 #ifdef __cplusplus
 }
 #endif
