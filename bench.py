@@ -30,7 +30,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s m
 # kernel mode ids (gd_engine.hip enums) -> readable names
 MODE_NAMES = {
     "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO"],
-    "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV"],
+    "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV",
+              "G_OTF_INIT", "G_INIT_W", "G_ITER"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
 }
@@ -42,26 +43,33 @@ def pretty(name):
     return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
 
 
-def kernel_bytes(name, L, last_frac=0.0):
+def kernel_bytes(name, L, n_iters):
     """Algorithmic HBM bytes per galaxy for one launch of a kernel (each compulsory input read once,
-    each output written once; see DESIGN.md 'Kernels and their rooflines')."""
+    each output written once), averaged over the launches of one forward where
+    the first / last ADMM iteration moves less."""
     img = L * L * 4                  # one fp32 image
     half = (L // 2 + 1) * L * 8      # one complex64 half spectrum
+    n = max(1, n_iters)
     k = pretty(name)
     table = {
-        f"k_row_fwd<{L},ITER>": 3 * img + 2 * half,          # z, u1, w -> T(2)
-        f"k_col<{L},ITER>": 5 * half,                        # T(2) + OTF -> T(2)
-        f"k_row_inv<{L},ITER>": 2 * half + 7 * img,          # T(2), z, u1, w, y -> u1, w, zin
-        f"k_row_fwd<{L},PSF_Y>": img + 2 * half,             # y (+ tiny psf) -> T(2)
-        f"k_col<{L},OTF_INIT>": 2 * half + 2 * half,         # T(2) -> OTF, T(1)
-        f"k_row_invfwd<{L},CLAMP>": 2 * half + img,          # T(1) -> zin, T(1)
-        f"k_col<{L},CONV>": 3 * half,                        # T(1) + OTF -> T(1)
-        f"k_row_inv<{L},INIT>": half + 4 * img,              # T(1), zin?, y -> u1, w
+        # Gaussian (spectral state): RF(z) -> C_G_ITER -> RI(zin)
+        f"k_row_fwd<{L},ONE>": img + half,                                  # z -> T
+        f"k_col<{L},G_ITER>": half * (7 + 8 * max(0, n - 2) + 4 * (n > 1)) / n,  # T,H,U1,W,F(y/a) -> U1,W,T
+        f"k_row_inv<{L},OUT1>": half + img,                                 # T -> zin | x
+        f"k_col<{L},G_OTF_INIT>": 2 * half + 3 * half,                      # T(2) -> OTF, F(y/a), T
+        f"k_col<{L},G_INIT_W>": 3 * half + half,                            # T, OTF, F(y/a) -> W
+        # Poisson (spatial u1, w): RF(z-u1, w) -> C_ITER -> RI_ITER
+        f"k_row_fwd<{L},ITER>": 3 * img + 2 * half,
+        f"k_col<{L},ITER>": 5 * half,
+        f"k_row_inv<{L},ITER>": ((2 * half + 7 * img) * (n - 1) + (2 * half + img)) / n,
+        f"k_col<{L},OTF_INIT>": 4 * half,
+        f"k_col<{L},CONV>": 3 * half,
+        f"k_row_inv<{L},INIT>": half + 3 * img,
+        # shared setup
+        f"k_row_fwd<{L},PSF_Y>": img + 2 * half,                            # y (+ 9 KB PSF) -> T(2)
+        f"k_row_invfwd<{L},CLAMP>": 2 * half + img,                         # T -> zin, T
     }
-    b = table.get(k)
-    if b is not None and k == f"k_row_inv<{L},ITER>" and last_frac:
-        b = b * (1 - last_frac) + (2 * half + img) * last_frac   # last iteration writes x only
-    return b
+    return table.get(k)
 
 
 def survey_bytes_per_galaxy(L, n, h=48):
@@ -83,6 +91,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--e2e-sample", type=int, default=64, help="galaxies for the ResUNet end-to-end sample")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--chunk-mb", type=float, default=None,
+                   help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
     return p.parse_args()
@@ -134,7 +144,11 @@ def main():
     dev = torch.device("cuda", local)
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
-    _lib.load()
+    lib = _lib.load()
+    if args.chunk_mb is not None:
+        lib.gd_set_chunk_bytes(int(args.chunk_mb * (1 << 20)))
+    chunk_bytes = lib.gd_set_chunk_bytes(0)
+    lib.gd_set_chunk_bytes(chunk_bytes)
 
     N, L, n = args.batch, args.size, args.n_iters
     obs, psf, alpha, _ = make_batch(N, L, seed=20250307 + rank, device=dev)
@@ -185,8 +199,7 @@ def main():
     kernels = {pretty(k): {"avg_ms": ms / c, "launches": c} for k, (ms, c) in kstats.items()}
     dom_raw = max(kstats, key=lambda k: kstats[k][0])
     dom_ms = kstats[dom_raw][0] / kstats[dom_raw][1]
-    last_frac = 1.0 / n if pretty(dom_raw) == f"k_row_inv<{L},ITER>" else 0.0
-    per_gal = kernel_bytes(dom_raw, L, last_frac)
+    per_gal = kernel_bytes(dom_raw, L, n)
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
     try:
@@ -213,7 +226,8 @@ def main():
                                f"(spectral engine: SubNet + OTF + init_l2 + {n} ADMM iterations), "
                                f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])",
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
-                   "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)"},
+                   "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
+                   "chunk_mib": chunk_bytes / (1 << 20)},
         "roofline": roofline,
         "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},

@@ -66,11 +66,16 @@ struct Args {
     float* o2;
     GalScalar alpha, rho1, rho2, rho2n;
     int llh;               // GD_LLH_GAUSSIAN / GD_LLH_POISSON
-    int last;              // final ADMM iteration: write x (times alpha for Poisson) to o2
+    int last;              // final ADMM iteration: write x (times alpha for Poisson)
+    int first;             // first ADMM iteration: spectral u1 is zero (not read)
+    float2* s_yal;         // Gaussian spectral state [N][K][L]: F(max(y,0)/alpha)
+    float2* s_u1;          //                                     F(u1)
+    float2* s_w;           //                                     F(v - u2)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO };
-enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV };
+enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV,
+               C_G_OTF_INIT, C_G_INIT_W, C_G_ITER };
 enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
 enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
@@ -89,8 +94,8 @@ struct Geo {
     static constexpr int RB = rows_per_block(LPB, L);  // rows per row-kernel block (even, divides L)
     static constexpr int RLD = L + 2;                  // row buffer leading dim (bank spread)
     static constexpr int XCH = xch_elems<L>();
-    // row kernels (worst case two images = RB lines): row buffer | exchange areas | result image
-    static constexpr int ROW_LDS = cmax(cmax(RB * RLD, RB * XCH), RB * L);
+    // row kernels (at most LPB lines): row buffer | exchange areas | staged / result images
+    static constexpr int ROW_LDS = cmax(cmax(LPB * RLD, LPB * XCH), LPB * L);
     static constexpr int COL_LDS = LPB * XCH;
     static_assert(L % RB == 0 && RB % 2 == 0, "rows per block must be even and divide L");
 };
@@ -125,7 +130,9 @@ __device__ __forceinline__ float v_step(int llh, float vt, float yp, float rho2,
 template <int L, int NI>
 struct RowGeo {
     using G = Geo<L>;
-    static constexpr int RB = G::RB;        // rows per block, per image (even, divides L)
+    // rows per block, per image (even, divides L): up to LPB lines (256 threads) per block, so a
+    // single-image kernel takes twice the rows of a two-image one
+    static constexpr int RB = rows_per_block(2 * G::LPB / NI, L);
     static constexpr int PAIRS = RB / 2;    // lines per image
     static constexpr int LINES = NI * PAIRS;
     static constexpr int THREADS = LINES * G::F1;
@@ -179,27 +186,41 @@ struct RfTraits {
     static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE) ? 1 : 2;
 };
 
-// Value of image `im` at pixel (r, c) for the RF producers.
+// Four consecutive pixels of image `im` starting at flat pixel index `pix` (row-major, 16-byte
+// aligned) for the RF producers; (r, c) locate the first of them inside the galaxy.
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int i, float x) {
+    if (i == 0) v.x = x; else if (i == 1) v.y = x; else if (i == 2) v.z = x; else v.w = x;
+}
+
 template <int L, int MODE>
-__device__ __forceinline__ float rf_source(const Args& a, int g, int im, int r, int c) {
-    const size_t pix = ((size_t)g * L + r) * L + c;
+__device__ __forceinline__ float4 rf_source4(const Args& a, int g, int im, int r, int c, size_t pix) {
     if constexpr (MODE == RF_ITER) {
-        return im == 0 ? a.a0[pix] - a.a1[pix] : a.a2[pix];          // z - u1 | v - u2
-    } else if constexpr (MODE == RF_PSF_Y) {
-        return im == 0 ? shifted_psf(a, g, r, c, L) : fmaxf(a.y[pix], 0.f) / a.alpha(g);
-    } else if constexpr (MODE == RF_PSF_YP) {
-        if (im == 0) return shifted_psf(a, g, r, c, L);
-        const float yp = fmaxf(a.y[pix], 0.f);
-        a.o0[pix] = yp;                                                // Richardson-Lucy x0
-        return yp;
-    } else if constexpr (MODE == RF_PSF_RAW) {
-        return im == 0 ? shifted_psf(a, g, r, c, L) : a.y[pix];
-    } else if constexpr (MODE == RF_PSF) {
-        return shifted_psf(a, g, r, c, L);
+        if (im == 0) {                                                 // z - u1
+            const float4 z = ld4(a.a0 + pix), u = ld4(a.a1 + pix);
+            return make_float4(z.x - u.x, z.y - u.y, z.z - u.z, z.w - u.w);
+        }
+        return ld4(a.a2 + pix);                                        // w = v - u2
+    } else if constexpr (MODE == RF_PSF || MODE == RF_PSF_Y || MODE == RF_PSF_YP || MODE == RF_PSF_RAW) {
+        if (im == 0)
+            return make_float4(shifted_psf(a, g, r, c, L), shifted_psf(a, g, r, c + 1, L),
+                               shifted_psf(a, g, r, c + 2, L), shifted_psf(a, g, r, c + 3, L));
+        const float4 y = ld4(a.y + pix);
+        if constexpr (MODE == RF_PSF_RAW) return y;
+        float4 yp = make_float4(fmaxf(y.x, 0.f), fmaxf(y.y, 0.f), fmaxf(y.z, 0.f), fmaxf(y.w, 0.f));
+        if constexpr (MODE == RF_PSF_YP) {
+            st4(a.o0 + pix, yp);                                       // Richardson-Lucy x0 = max(y, 0)
+            return yp;
+        } else {
+            const float al = a.alpha(g);                               // max(y,0) / alpha
+            return make_float4(yp.x / al, yp.y / al, yp.z / al, yp.w / al);
+        }
     } else if constexpr (MODE == RF_ONE) {
-        return a.a0[pix];
+        return ld4(a.a0 + pix);
     } else {
-        return im == 0 ? a.a0[pix] : a.a1[pix];
+        return ld4((im == 0 ? a.a0 : a.a1) + pix);
     }
 }
 
@@ -210,24 +231,32 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI>::THREADS)) void k_ro
     using R = RowGeo<L, NI>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
     const int tid = threadIdx.x;
     const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
     const int row0 = (blockIdx.x - g * blocks_per_g) * R::RB;
     const int line = tid / F1, j = tid - line * F1;
     const int im = line / R::PAIRS, m = line - im * R::PAIRS;
-    const int rA = row0 + 2 * m;
     fill_twiddles<L>(tw, tid, R::THREADS);
+    // stage the block's RB rows of each image through LDS with 16-byte coalesced loads
+    float* stage = reinterpret_cast<float*>(lds);  // [im][rr][c]
+    for (int q = tid * 4; q < NI * R::RB * L; q += R::THREADS * 4) {
+        const int imq = q / (R::RB * L), rem = q - imq * (R::RB * L);
+        const int rr = rem / L, c = rem - rr * L;
+        const size_t pix = ((size_t)g * L + row0 + rr) * L + c;
+        st4(stage + q, rf_source4<L, MODE>(a, g, imq, row0 + rr, c, pix));
+    }
+    __syncthreads();
     float2 v[F2];
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int c = j + F1 * s;
-        v[s] = make_float2(rf_source<L, MODE>(a, g, im, rA, c), rf_source<L, MODE>(a, g, im, rA + 1, c));
+        v[s] = make_float2(stage[(im * R::RB + 2 * m) * L + c], stage[(im * R::RB + 2 * m + 1) * L + c]);
     }
-    __syncthreads();  // twiddles
+    __syncthreads();  // staging -> exchange areas
     line_fft<L, false>(v, j, lds + line * G::XCH, tw);
-    __syncthreads();  // exchange area -> row buffer
+    __syncthreads();  // exchange areas -> row buffer
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
@@ -238,11 +267,13 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI>::THREADS)) void k_ro
 template <int MODE>
 struct ColTraits {
     static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
-                                 MODE == C_WIENER || MODE == C_CONV2);
+                                 MODE == C_WIENER || MODE == C_CONV2 || MODE == C_G_OTF_INIT);
     static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
-    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD);
-    static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
-    static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2);
+    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_INIT_W);
+    static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF ||
+                                       MODE == C_G_OTF_INIT);
+    static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2 ||
+                                      MODE == C_G_INIT_W || MODE == C_G_ITER);
     static constexpr bool FWD = (MODE != C_INV);
 };
 
@@ -276,9 +307,11 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
-    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER) ? a.alpha(g) : 1.f;
-    const float r1 = (MODE == C_ITER) ? a.rho1(g) : 0.f;
-    const float r2 = (MODE == C_ITER) ? a.rho2(g) : 0.f;
+    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_OTF_INIT) ? a.alpha(g) : 1.f;
+    const float r1 = (MODE == C_ITER || MODE == C_G_ITER) ? a.rho1(g) : 0.f;
+    const float r2 = (MODE == C_ITER || MODE == C_G_ITER) ? a.rho2(g) : 0.f;
+    const bool glast = (MODE == C_G_ITER) && a.last;
+    const float r2n = (MODE == C_G_INIT_W || (MODE == C_G_ITER && !glast)) ? a.rho2n(g) : 0.f;
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
@@ -304,6 +337,50 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float lhs = HtH + 1.0f / al;
             const float2 rhs = cmulc(Q[s], Hk);
             P[s] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
+        } else if constexpr (MODE == C_G_OTF_INIT) {
+            // as C_OTF_INIT, and keep F(y/alpha) as Gaussian spectral state
+            if (valid) a.s_yal[ob + ky] = Q[s];
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float lhs = HtH + 1.0f / al;
+            const float2 rhs = cmulc(Q[s], Hk);
+            P[s] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
+        } else if constexpr (MODE == C_G_INIT_W) {
+            // first V step in the spectral domain (u1 = u2 = 0): W1 = V1 = (rho2 (H X0 + 0) + F(y/alpha)) / (1 + rho2)
+            const float2 HX = cmul(Hk, P[s]);
+            const float2 Ya = a.s_yal[ob + ky];
+            const float d = 1.0f + r2n;
+            if (valid) a.s_w[ob + ky] = make_float2((r2n * HX.x + Ya.x) / d, (r2n * HX.y + Ya.y) / d);
+        } else if constexpr (MODE == C_G_ITER) {
+            // Gaussian ADMM iteration entirely in the spectral domain (all steps of
+            // models/Unrolled_ADMM.py:207-213 are linear for llh='Gaussian'):
+            //   X   = (rho1 (Z - U1) + rho2 conj(H) W) / (rho1 |H|^2 + rho2)      runtime X_Update :315-319
+            //   U1' = (U1 + X) - Z ;  U2' = H X - W                               :212-213 (W = V - U2)
+            //   V'  = (rho2' (H X + U2') + F(y/alpha)) / (1 + rho2') ;  W' = V' - U2'   V step :335-336
+            //   out = X + U1' (next denoiser input)  |  X (last iteration)
+            const float2 Zk = P[s];
+            const float2 U1 = a.first ? make_float2(0.f, 0.f) : a.s_u1[ob + ky];
+            const float2 Wk = a.s_w[ob + ky];
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float lhs = r1 * HtH + r2;
+            const float2 A = csub(Zk, U1);
+            const float2 HtW = cmulc(Wk, Hk);
+            const float2 rhs = make_float2(r1 * A.x + r2 * HtW.x, r1 * A.y + r2 * HtW.y);
+            const float2 X = make_float2(rhs.x / lhs, rhs.y / lhs);
+            if (glast) {
+                P[s] = cscale(X, inv_n);
+            } else {
+                const float2 U1n = csub(cadd(U1, X), Zk);
+                const float2 HX = cmul(Hk, X);
+                const float2 U2n = csub(HX, Wk);
+                const float2 Ya = a.s_yal[ob + ky];
+                const float d = 1.0f + r2n;
+                const float2 Vn = make_float2((r2n * (HX.x + U2n.x) + Ya.x) / d, (r2n * (HX.y + U2n.y) + Ya.y) / d);
+                if (valid) {
+                    a.s_u1[ob + ky] = U1n;
+                    a.s_w[ob + ky] = csub(Vn, U2n);
+                }
+                P[s] = cscale(cadd(X, U1n), inv_n);
+            }
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
@@ -346,13 +423,6 @@ template <int MODE>
 struct RiTraits {
     static constexpr int NI = (MODE == RI_ITER || MODE == RI_OUT2) ? 2 : 1;
 };
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-__device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
-__device__ __forceinline__ void f4set(float4& v, int i, float x) {
-    if (i == 0) v.x = x; else if (i == 1) v.y = x; else if (i == 2) v.z = x; else v.w = x;
-}
 
 template <int L, int MODE>
 __global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI>::THREADS)) void k_row_inv(Args a) {
@@ -573,7 +643,8 @@ struct ProfScope {
 template <int L>
 struct Launcher {
     using G = Geo<L>;
-    static int row_grid(int N) { return N * (L / G::RB); }
+    template <int NI>
+    static int row_grid(int N) { return N * (L / RowGeo<L, NI>::RB); }
     static int col_grid(int N) { return (N * G::K + G::LPB - 1) / G::LPB; }
     static std::string nm(const char* k, int mode) {
         return std::string(k) + "<" + std::to_string(L) + "," + std::to_string(mode) + ">";
@@ -582,7 +653,7 @@ struct Launcher {
     template <int MODE>
     static int rf(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kRowFwdName, MODE), st);
-        hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, RfTraits<MODE>::NI>::THREADS), 0, st, a);
+        hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid<RfTraits<MODE>::NI>(a.N)), dim3(RowGeo<L, RfTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_fwd");
     }
     template <int MODE>
@@ -594,13 +665,13 @@ struct Launcher {
     template <int MODE>
     static int ri(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kRowInvName, MODE), st);
-        hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, RiTraits<MODE>::NI>::THREADS), 0, st, a);
+        hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid<RiTraits<MODE>::NI>(a.N)), dim3(RowGeo<L, RiTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_inv");
     }
     template <int MODE>
     static int rif(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kRowInvFwdName, MODE), st);
-        hipLaunchKernelGGL((k_row_invfwd<L, MODE>), dim3(row_grid(a.N)), dim3(RowGeo<L, 1>::THREADS), 0, st, a);
+        hipLaunchKernelGGL((k_row_invfwd<L, MODE>), dim3(row_grid<1>(a.N)), dim3(RowGeo<L, 1>::THREADS), 0, st, a);
         return check_launch("k_row_invfwd");
     }
 };
@@ -611,9 +682,54 @@ struct Launcher {
         if (_rc != GD_OK) return _rc; \
     } while (0)
 
+// ---------------------------------------------------------------- Infinity-Cache chunking
+// A multi-kernel operation runs chunk by chunk over the batch: each chunk's spectral workspace
+// (and the images the row passes read twice) stays resident in the 256 MiB Infinity Cache between
+// its kernels instead of round-tripping through HBM.  g_chunk_bytes is the target resident working
+// set per chunk (0 = whole batch in one pass).
+size_t g_chunk_bytes = 0;  // measured: chunking slower at 256^2 (small-grid fill/drain > MALL gain)
+
+inline Args offset_args(const Args& a, int g0, int n, int L) {
+    Args b = a;
+    b.N = n;
+    const size_t img = (size_t)g0 * L * L;
+    const size_t spec = (size_t)g0 * (L / 2 + 1) * L;
+    if (b.otf) b.otf += spec;
+    if (b.s_yal) b.s_yal += spec;
+    if (b.s_u1) b.s_u1 += spec;
+    if (b.s_w) b.s_w += spec;
+    if (b.y) b.y += img;
+    if (b.a0) b.a0 += img;
+    if (b.a1) b.a1 += img;
+    if (b.a2) b.a2 += img;
+    if (b.o0) b.o0 += img;
+    if (b.o1) b.o1 += img;
+    if (b.o2) b.o2 += img;
+    if (b.psf) b.psf += (long long)g0 * a.psf_gstride;
+    GalScalar* gs[] = {&b.alpha, &b.rho1, &b.rho2, &b.rho2n};
+    for (GalScalar* x : gs)
+        if (x->p) x->p += (long long)g0 * x->stride;
+    return b;  // T (workspace) is not offset: every chunk reuses its head
+}
+
+template <typename F>
+int for_chunks(const Args& a, int L, size_t per_galaxy_bytes, F&& f) {
+    int G = a.N;
+    if (g_chunk_bytes && per_galaxy_bytes) {
+        const size_t g = g_chunk_bytes / per_galaxy_bytes;
+        G = (int)(g < 1 ? 1 : (g > (size_t)a.N ? (size_t)a.N : g));
+    }
+    for (int g0 = 0; g0 < a.N; g0 += G) {
+        const int n = (a.N - g0 < G) ? a.N - g0 : G;
+        GD_TRY(f(offset_args(a, g0, n, L)));
+    }
+    return GD_OK;
+}
+
 // Operation bodies, templated on L.
 template <int L>
 struct Ops {
+    static constexpr size_t IMG = (size_t)L * L * 4, HALF = (size_t)(L / 2 + 1) * L * 8;
     using Lc = Launcher<L>;
     static int psf_to_otf(Args a, hipStream_t st) {
         GD_TRY(Lc::template rf<RF_PSF>(a, st));
@@ -632,42 +748,70 @@ struct Ops {
         GD_TRY(Lc::template col<C_INV>(a, st));
         return Lc::template ri<RI_OUT1>(a, st);
     }
-    static int admm_init(Args a, hipStream_t st) {
+    static int admm_init(Args a0, hipStream_t st) {
         // a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
-        Args b = a;
-        GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
-        GD_TRY(Lc::template col<C_OTF_INIT>(b, st));
-        b.o0 = a.o2;  // RIF_CLAMP writes x0 -> zin
-        GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
-        GD_TRY(Lc::template col<C_CONV>(b, st));
-        return Lc::template ri<RI_INIT>(a, st);
+        return for_chunks(a0, L, 2 * HALF + 4 * IMG, [&](const Args& a) {
+            Args b = a;
+            GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
+            GD_TRY(Lc::template col<C_OTF_INIT>(b, st));
+            b.o0 = a.o2;  // RIF_CLAMP writes x0 -> zin
+            GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
+            GD_TRY(Lc::template col<C_CONV>(b, st));
+            return Lc::template ri<RI_INIT>(a, st);
+        });
     }
-    static int admm_iter(Args a, hipStream_t st) {
+    static int admm_init_gauss(Args a0, hipStream_t st) {
+        // spectral state: otf, s_yal, s_w (s_u1 implicitly 0); a.o2 = zin (x0)
+        return for_chunks(a0, L, 2 * HALF + 4 * IMG, [&](const Args& a) {
+            Args b = a;
+            GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
+            GD_TRY(Lc::template col<C_G_OTF_INIT>(b, st));
+            b.o0 = a.o2;  // RIF_CLAMP writes x0 -> zin
+            GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
+            return Lc::template col<C_G_INIT_W>(b, st);
+        });
+    }
+    static int admm_iter_gauss(Args a0, hipStream_t st) {
+        // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
+        return for_chunks(a0, L, HALF + 2 * IMG, [&](const Args& a) {
+            GD_TRY(Lc::template rf<RF_ONE>(a, st));
+            GD_TRY(Lc::template col<C_G_ITER>(a, st));
+            return Lc::template ri<RI_OUT1>(a, st);
+        });
+    }
+    static int admm_iter(Args a0, hipStream_t st) {
         // a.a0 = z, a.a1 = u1 (RF reads), a.a2 = w; RI: a.o0 = u1, a.o1 = w, a.o2 = zin / out
-        GD_TRY(Lc::template rf<RF_ITER>(a, st));
-        GD_TRY(Lc::template col<C_ITER>(a, st));
-        return Lc::template ri<RI_ITER>(a, st);
+        return for_chunks(a0, L, 2 * HALF + 3 * IMG, [&](const Args& a) {
+            GD_TRY(Lc::template rf<RF_ITER>(a, st));
+            GD_TRY(Lc::template col<C_ITER>(a, st));
+            return Lc::template ri<RI_ITER>(a, st);
+        });
     }
-    static int wiener(Args a, hipStream_t st) {
-        GD_TRY(Lc::template rf<RF_PSF_RAW>(a, st));
-        GD_TRY(Lc::template col<C_WIENER>(a, st));
-        return Lc::template ri<RI_OUT1>(a, st);
+    static int wiener(Args a0, hipStream_t st) {
+        return for_chunks(a0, L, 2 * HALF + IMG, [&](const Args& a) {
+            GD_TRY(Lc::template rf<RF_PSF_RAW>(a, st));
+            GD_TRY(Lc::template col<C_WIENER>(a, st));
+            return Lc::template ri<RI_OUT1>(a, st);
+        });
     }
-    static int richardson_lucy(Args a, int n_iters, hipStream_t st) {
-        // a.o0 = x (output, also the iterate); otf kept in a.otf
-        GD_TRY(Lc::template rf<RF_PSF_YP>(a, st));
-        if (n_iters <= 0) return GD_OK;
-        GD_TRY(Lc::template col<C_OTF_CONV>(a, st));
-        for (int it = 0; it < n_iters; ++it) {
-            if (it > 0) GD_TRY(Lc::template col<C_CONV>(a, st));
-            GD_TRY(Lc::template rif<RIF_RL_RATIO>(a, st));
-            GD_TRY(Lc::template col<C_CONVC>(a, st));
-            if (it + 1 < n_iters)
-                GD_TRY(Lc::template rif<RIF_RL_UPDATE>(a, st));
-            else
-                GD_TRY(Lc::template ri<RI_RL_FINAL>(a, st));
-        }
-        return GD_OK;
+    static int richardson_lucy(Args a0, int n_iters, hipStream_t st) {
+        // a.o0 = x (output, also the iterate); otf kept in a.otf.  The whole iteration loop runs per
+        // chunk, so x, y, the OTF and the workspace stay cache-resident across all n_iters.
+        return for_chunks(a0, L, 2 * HALF + 2 * IMG, [&](const Args& a) {
+            GD_TRY(Lc::template rf<RF_PSF_YP>(a, st));
+            if (n_iters <= 0) return GD_OK;
+            GD_TRY(Lc::template col<C_OTF_CONV>(a, st));
+            for (int it = 0; it < n_iters; ++it) {
+                if (it > 0) GD_TRY(Lc::template col<C_CONV>(a, st));
+                GD_TRY(Lc::template rif<RIF_RL_RATIO>(a, st));
+                GD_TRY(Lc::template col<C_CONVC>(a, st));
+                if (it + 1 < n_iters)
+                    GD_TRY(Lc::template rif<RIF_RL_UPDATE>(a, st));
+                else
+                    GD_TRY(Lc::template ri<RI_RL_FINAL>(a, st));
+            }
+            return GD_OK;
+        });
     }
 };
 
@@ -776,10 +920,33 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::irfft2(a, (hipStream_t)stream); });
 }
 
+size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
+    if (!gd_supported_size(H, W) || N <= 0) return 0;
+    const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
+    return llh == GD_LLH_GAUSSIAN ? 4 * spec : spec + 2 * img;
+}
+
+namespace {
+// state layout - Gaussian: [otf | F(y/alpha) | F(u1) | F(v-u2)] (spectral); Poisson: [otf | u1 | w]
+void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
+    const size_t spec = (size_t)N * (W / 2 + 1) * H;
+    float2* base = reinterpret_cast<float2*>(state);
+    a.otf = base;
+    if (llh == GD_LLH_GAUSSIAN) {
+        a.s_yal = base + spec;
+        a.s_u1 = base + 2 * spec;
+        a.s_w = base + 3 * spec;
+    } else {
+        float* u1 = reinterpret_cast<float*>(base + spec);
+        a.o0 = u1;                       // u1 (spatial)
+        a.o1 = u1 + (size_t)N * H * W;   // w = v - u2 (spatial)
+    }
+}
+}  // namespace
+
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
-                 int llh, int N, int H, int W, void* otf_half, float* u1, float* wv, float* zin,
-                 void* ws, void* stream) {
+                 int llh, int N, int H, int W, void* state, float* zin, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
     GD_TRY(check_psf(h, w, H));
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
@@ -789,31 +956,39 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     a.alpha = GalScalar{alpha, alpha_stride};
     a.rho2n = GalScalar{rho2, rho2_stride};
     a.llh = llh;
-    a.otf = reinterpret_cast<float2*>(otf_half);
-    a.o0 = u1; a.o1 = wv; a.o2 = zin;
+    bind_state(a, state, N, H, W, llh);
+    a.o2 = zin;
+    if (llh == GD_LLH_GAUSSIAN)
+        return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
 }
 
-int gd_admm_iter(const float* y, const void* otf_half, const float* z, float* u1, float* wv,
-                 float* zin_or_out, const float* alpha, long long alpha_stride, const float* rho1,
-                 long long rho1_stride, const float* rho2, long long rho2_stride,
-                 const float* rho2_next, long long rho2_next_stride, int llh, int last, int N, int H,
-                 int W, void* ws, void* stream) {
+int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float* alpha, long long alpha_stride,
+                 const float* rho1, long long rho1_stride, const float* rho2, long long rho2_stride,
+                 const float* rho2_next, long long rho2_next_stride, int llh, int iter, int last, int N, int H,
+                 int W, void* state, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
     if (N == 0) return GD_OK;
     if (!last && rho2_next == nullptr) return fail(GD_ERR_ARG, "rho2_next required unless last");
     Args a = base_args(N, ws, H);
     a.y = y;
-    a.otf = reinterpret_cast<float2*>(const_cast<void*>(otf_half));
-    a.a0 = z; a.a1 = u1; a.a2 = wv;
-    a.o0 = u1; a.o1 = wv; a.o2 = zin_or_out;
+    bind_state(a, state, N, H, W, llh);
     a.alpha = GalScalar{alpha, alpha_stride};
     a.rho1 = GalScalar{rho1, rho1_stride};
     a.rho2 = GalScalar{rho2, rho2_stride};
     a.rho2n = GalScalar{rho2_next ? rho2_next : rho2, rho2_next ? rho2_next_stride : rho2_stride};
     a.llh = llh;
     a.last = last;
+    a.first = iter == 0;
+    if (llh == GD_LLH_GAUSSIAN) {
+        a.a0 = z;
+        a.o0 = zin_or_out;
+        return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter_gauss(a, (hipStream_t)stream); });
+    }
+    // Poisson: spatial u1 / w (RF reads z, u1, w; RI writes u1, w and zin_or_out)
+    a.a0 = z; a.a1 = a.o0; a.a2 = a.o1;
+    a.o2 = zin_or_out;
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter(a, (hipStream_t)stream); });
 }
 
@@ -882,6 +1057,12 @@ int gd_profile_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_stats.clear();
     return GD_OK;
+}
+
+size_t gd_set_chunk_bytes(size_t bytes) {
+    const size_t old = g_chunk_bytes;
+    g_chunk_bytes = bytes;
+    return old;
 }
 
 }  // extern "C"

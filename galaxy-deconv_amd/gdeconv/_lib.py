@@ -31,11 +31,13 @@ SIGNATURES = {
     "gd_conv_fft_batch": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _P]),
     "gd_rfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
-    "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
-    "gd_admm_iter": (_I, [_P, _P, _P, _P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I,
-                          _P, _P]),
+    "gd_admm_state_bytes": (_SZ, [_I, _I, _I, _I]),
+    "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "gd_admm_iter": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P,
+                          _P]),
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
+    "gd_set_chunk_bytes": (_SZ, [_SZ]),
     "gd_profile_enable": (_I, [_I]),
     "gd_profile_collect": (_I, []),
     "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),
@@ -62,7 +64,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gd_abi_version() != 1:
+    if lib.gd_abi_version() != 2:
         raise EngineError("libgdeconv.so ABI version mismatch")
     _lib = lib
     return lib

@@ -160,7 +160,9 @@ def richardson_lucy(y, psf, n_iters):
 
 
 class ADMMState:
-    """Device state of one unrolled-ADMM forward: u1, w = v - u2, zin (next denoiser input), OTF."""
+    """Device state of one unrolled-ADMM forward: the engine's opaque state buffer (OTF + u1 and
+    v - u2, spectral for llh='Gaussian', spatial for 'Poisson') and ``zin``, the next denoiser
+    input (x + u1)."""
 
     def __init__(self, y, psf, alpha, llh):
         _require_device(y, psf, alpha)
@@ -173,11 +175,17 @@ class ADMMState:
             raise ValueError("llh must be 'Gaussian' or 'Poisson'")
         self.llh = _lib.GD_LLH[llh]
         dev = self.y.device
-        self.u1 = torch.empty_like(self.y)
-        self.wv = torch.empty_like(self.y)
+        nbytes = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W, self.llh))
+        self.ws = workspace(self.N, self.H, self.W, dev)   # validates the size first
+        self.state = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.zin = torch.empty_like(self.y)
-        self.otf = empty_otf(self.N, self.H, self.W, dev)
-        self.ws = workspace(self.N, self.H, self.W, dev)
+        self.iter = 0
+
+    @property
+    def otf(self):
+        """Half-spectrum OTF [N, W//2+1, H] (a view of the state buffer)."""
+        K = self.W // 2 + 1
+        return self.state[: self.N * K * self.H * 8].view(torch.complex64).view(self.N, K, self.H)
 
     def init(self, rho2_first):
         """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; rho2_first = (tensor, stride)."""
@@ -185,9 +193,9 @@ class ADMMState:
         k = self.psf
         _lib.check(self.lib.gd_admm_init(
             self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
-            self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.otf.data_ptr(),
-            self.u1.data_ptr(), self.wv.data_ptr(), self.zin.data_ptr(), self.ws.data_ptr(), _stream()),
-            "gd_admm_init")
+            self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.state.data_ptr(),
+            self.zin.data_ptr(), self.ws.data_ptr(), _stream()), "gd_admm_init")
+        self.iter = 0
 
     def step(self, z, rho1, rho2, rho2_next, out=None):
         """One loop body (models/Unrolled_ADMM.py:207-213) after the denoiser returned ``z``.
@@ -202,10 +210,11 @@ class ADMMState:
         r2, r2s = rho2
         rn, rns = (rho2_next if rho2_next is not None else (None, 0))
         _lib.check(self.lib.gd_admm_iter(
-            self.y.data_ptr(), self.otf.data_ptr(), z.data_ptr(), self.u1.data_ptr(), self.wv.data_ptr(),
-            dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s, r1.data_ptr(), r1s, r2.data_ptr(), r2s,
-            None if rn is None else rn.data_ptr(), rns, self.llh, int(last), self.N, self.H, self.W,
-            self.ws.data_ptr(), _stream()), "gd_admm_iter")
+            self.y.data_ptr(), z.data_ptr(), dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s,
+            r1.data_ptr(), r1s, r2.data_ptr(), r2s, None if rn is None else rn.data_ptr(), rns, self.llh,
+            self.iter, int(last), self.N, self.H, self.W, self.state.data_ptr(), self.ws.data_ptr(),
+            _stream()), "gd_admm_iter")
+        self.iter += 1
         return dst
 
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GD_ABI_VERSION 1
+#define GD_ABI_VERSION 2
 
 #define GD_OK 0
 #define GD_ERR_ARG (-1)
@@ -62,24 +62,26 @@ int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out
 int gd_rfft2(const float* x, void* spec, int N, int H, int W, void* stream);
 int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
 
-/* ADMM setup: OTF, x0 = clamp(init_l2), u1 = 0, u2 = 0, first V step.
- * Outputs: otf_half, u1 (zeros), wv = v1 - u2 (= v1), zin = x0 (= x0 + u1, the first denoiser input).
- * rho2 = the first iteration's rho2 (rho2_iters[..., 0]). */
+/* Unrolled ADMM.  The per-forward state lives in an opaque device buffer of
+ * gd_admm_state_bytes(N,H,W,llh) bytes whose first gd_otf_bytes(N,H,W) bytes are the half-spectrum
+ * OTF.  llh = GD_LLH_GAUSSIAN keeps u1, v - u2 and F(max(y,0)/alpha) in the SPECTRAL domain (every
+ * step of the Gaussian iteration is linear, so one forward and one inverse transform per iteration
+ * suffice); GD_LLH_POISSON (sqrt in the V step) keeps u1 and v - u2 as images.
+ *
+ * gd_admm_init: OTF, x0 = clamp(init_l2) -> zin (the first denoiser input, x0 + u1 with u1 = 0),
+ *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].
+ * gd_admm_iter: one loop body after the denoiser produced z from zin (iter = 0-based index):
+ *               X update, duals, then (unless last) the next V step with rho2_next and the next
+ *               denoiser input x + u1 -> zin_or_out; last != 0 -> zin_or_out = x (times alpha for
+ *               Poisson).  z may alias zin_or_out (identity denoiser). */
+size_t gd_admm_state_bytes(int N, int H, int W, int llh);
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
-                 int llh, int N, int H, int W, void* otf_half, float* u1, float* wv, float* zin,
-                 void* ws, void* stream);
-
-/* One ADMM iteration after the denoiser produced z from zin:
- *   X-update, u1 += x - z, u2 += conv(H,x) - v, then (unless last) the next V step with rho2_next
- *   -> u1, wv = v_next - u2, zin_or_out = x + u1 (next denoiser input);
- *   last != 0 -> zin_or_out = x (times alpha for Poisson), u1 / wv untouched.
- * z may alias zin_or_out (identity denoiser). */
-int gd_admm_iter(const float* y, const void* otf_half, const float* z, float* u1, float* wv,
-                 float* zin_or_out, const float* alpha, long long alpha_stride, const float* rho1,
-                 long long rho1_stride, const float* rho2, long long rho2_stride,
-                 const float* rho2_next, long long rho2_next_stride, int llh, int last, int N, int H,
-                 int W, void* ws, void* stream);
+                 int llh, int N, int H, int W, void* state, float* zin, void* ws, void* stream);
+int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float* alpha, long long alpha_stride,
+                 const float* rho1, long long rho1_stride, const float* rho2, long long rho2_stride,
+                 const float* rho2_next, long long rho2_next_stride, int llh, int iter, int last, int N, int H,
+                 int W, void* state, void* ws, void* stream);
 
 /* x = Re IFFT2(conj(H) FFT2(y) / (|H|^2 + 350/alpha)). */
 int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
@@ -88,6 +90,12 @@ int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, in
 /* Richardson-Lucy from x0 = max(y,0); otf_half receives the OTF (gd_otf_bytes). */
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
+
+/* Infinity-Cache chunking: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
+ * run over the batch in chunks whose working set is about `bytes` (default 96 MiB), so spectra stay
+ * resident in the 256 MiB Infinity Cache between kernels.  0 = whole batch per kernel.  Returns the
+ * previous value.  Process-wide; set it before enqueuing work. */
+size_t gd_set_chunk_bytes(size_t bytes);
 
 /* Opt-in per-kernel timing: when enabled, every kernel launch is bracketed by hipEvents on its
  * stream.  gd_profile_collect() waits for them and returns the number of distinct kernels;

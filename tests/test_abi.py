@@ -49,7 +49,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_host_only_queries(lib):
-    assert lib.gd_abi_version() == 1
+    assert lib.gd_abi_version() == 2
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
     assert lib.gd_supported_size(50, 50) == 0 and lib.gd_supported_size(256, 128) == 0
     # workspace: N * 2 images * (W/2+1) * H complex64
@@ -63,4 +63,7 @@ def test_argument_errors_need_no_device(lib):
     assert b"even" in lib.gd_last_error()
     assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 50, 50, None, None) == -2
     assert lib.gd_admm_init(None, None, 0, 48, 48, None, 0, None, 0, 7, 1, 48, 48,
-                            None, None, None, None, None, None) == -1
+                            None, None, None, None) == -1
+    # state: Gaussian keeps OTF + F(y/alpha) + F(u1) + F(v-u2); Poisson OTF + two images
+    assert lib.gd_admm_state_bytes(3, 48, 48, 0) == 4 * 3 * 25 * 48 * 8
+    assert lib.gd_admm_state_bytes(3, 48, 48, 1) == 3 * 25 * 48 * 8 + 2 * 3 * 48 * 48 * 4

@@ -87,3 +87,19 @@ def test_shard_range_covers_batch():
             assert parts[0][0] == 0 and parts[-1][1] == N
             assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
             assert max(b - a for a, b in parts) - min(b - a for a, b in parts) <= 1
+
+
+def test_subnet_bn_folding_matches_reference_order():
+    from gdeconv.nets import SubNet
+    from gdeconv.weights import make_state_dict
+    from gdeconv.synth import make_batch
+    net = SubNet(8)
+    net.load_state_dict(make_state_dict(net, 3))
+    net.eval()
+    _, psf, alpha, _ = make_batch(6, 64, seed=2)
+    with torch.no_grad():
+        a1, a2 = net.set_fold_bn(False)(psf, alpha)
+        b1, b2 = net.set_fold_bn(True)(psf, alpha)
+        c1, _ = net(psf, alpha)          # cached folded weights reused
+    assert torch.allclose(a1, b1, rtol=2e-5, atol=1e-7) and torch.allclose(a2, b2, rtol=2e-5, atol=1e-7)
+    assert torch.equal(b1, c1)

@@ -55,6 +55,7 @@ def _denoiser_and_subnet(n):
 
     m = M()
     m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    m.init.set_fold_bn(False)   # reference op order: conv -> BN -> ReLU
     return m.eval()
 
 
