@@ -40,6 +40,7 @@
 
 #include "../../include/gdeconv.h"
 #include "gd_fft.hpp"
+#include "gd_subnet.hpp"
 
 namespace gd {
 
@@ -277,7 +278,9 @@ struct ColTraits {
     static constexpr bool FWD = (MODE != C_INV);
 };
 
-template <int L, int MODE>
+// VAR: experiment switch for tools/kbench.hip (0 = production; 1 = no FFTs, memory only;
+// 2 = G_ITER operands H and W loaded before the forward FFT)
+template <int L, int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) void k_col(Args a) {
     using G = Geo<L>;
     using TR = ColTraits<MODE>;
@@ -300,8 +303,17 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         P[s] = a.T[c0 + j + F1 * s];
         if constexpr (TR::IN2) Q[s] = a.T[c1 + j + F1 * s];
     }
+    float2 Hpre[VAR == 2 ? F2 : 1], Wpre[VAR == 2 ? F2 : 1];
+    if constexpr (VAR == 2 && MODE == C_G_ITER) {
+        const size_t ob0 = ((size_t)g * K + kx) * L;
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            Hpre[s] = a.otf[ob0 + j + F1 * s];
+            Wpre[s] = a.s_w[ob0 + j + F1 * s];
+        }
+    }
     __syncthreads();  // twiddles
-    if constexpr (TR::FWD) {
+    if constexpr (TR::FWD && VAR != 1) {
         line_fft<L, false>(P, j, my, tw);
         if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
     }
@@ -316,7 +328,8 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
         float2 Hk = make_float2(0.f, 0.f);
-        if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
+        if constexpr (VAR == 2 && MODE == C_G_ITER) Hk = Hpre[s];
+        else if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
         if constexpr (TR::STORE_OTF || MODE == C_WIENER) Hk = P[s];
         if constexpr (TR::STORE_OTF) {
             if (valid) a.otf[ob + ky] = Hk;
@@ -359,7 +372,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             //   out = X + U1' (next denoiser input)  |  X (last iteration)
             const float2 Zk = P[s];
             const float2 U1 = a.first ? make_float2(0.f, 0.f) : a.s_u1[ob + ky];
-            const float2 Wk = a.s_w[ob + ky];
+            float2 Wk;
+            if constexpr (VAR == 2) Wk = Wpre[s];
+            else Wk = a.s_w[ob + ky];
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
             const float lhs = r1 * HtH + r2;
             const float2 A = csub(Zk, U1);
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             P[s] = cscale(P[s], inv_n);
         }
     }
-    if constexpr (TR::HAS_OUT && MODE != C_FWD) {
+    if constexpr (TR::HAS_OUT && MODE != C_FWD && VAR != 1) {
         line_fft<L, true>(P, j, my, tw);
         if constexpr (TR::OUT2) line_fft<L, true>(Q, j, my, tw);
     }
@@ -1063,6 +1078,17 @@ size_t gd_set_chunk_bytes(size_t bytes) {
     const size_t old = g_chunk_bytes;
     g_chunk_bytes = bytes;
     return old;
+}
+
+int gd_subnet_param_count(void) { return gd::subnet::kParams; }
+
+int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream) {
+    if (N < 0) return fail(GD_ERR_ARG, "negative batch");
+    if (N == 0) return GD_OK;
+    ProfScope ps("k_subnet_features<128,0>", (hipStream_t)stream);
+    hipLaunchKernelGGL(gd::subnet::k_subnet_features, dim3(N), dim3(gd::subnet::kThreads), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float2*>(otf128_half), params, feat, N);
+    return check_launch("k_subnet_features");
 }
 
 }  // extern "C"

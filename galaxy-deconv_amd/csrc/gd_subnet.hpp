@@ -1,0 +1,140 @@
+// SubNet feature extractor (models/Unrolled_ADMM.py:77-84) as ONE kernel, one workgroup per galaxy.
+//
+//   |FFT2(pad128(psf))|^2 -> MaxPool2 -> [conv3x3+BN+ReLU] x2 -> MaxPool2 -> ... (4 Down blocks)
+//   -> 16 x 8 x 8 = 1024 features (channel-major, the reference's .view(N, 1, 16*8*8) order)
+//
+// Input is the engine's half-spectrum OTF of the PSF at 128x128 (gd_psf_to_otf): a circular shift
+// only changes phases, so |OTF|^2 equals |FFT2(F.pad(psf))|^2 of :79-83; the full 128 x 128 map is
+// read through Hermitian symmetry |H(ky,kx)|^2 = |H(-ky,-kx)|^2.  BatchNorm (eval) is folded into
+// the conv weights on the host.  Activations live in LDS (80 KiB: two workgroups per CU); a thread
+// owns an output pixel and a block of its output channels in registers, so each input value is
+// read once per channel block and the weights are wave-uniform (scalar loads).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gd {
+namespace subnet {
+
+// conv layer table: (cin, cout, spatial side)
+constexpr int kCin[8] = {1, 4, 4, 8, 8, 16, 16, 16};
+constexpr int kCout[8] = {4, 4, 8, 8, 16, 16, 16, 16};
+constexpr int woff(int l) {  // offset of layer l's weights in the packed [w | b] array
+    int o = 0;
+    for (int i = 0; i < l; ++i) o += kCout[i] * kCin[i] * 9 + kCout[i];
+    return o;
+}
+constexpr int kParams = woff(8);  // 9,172 floats
+constexpr int kThreads = 256;
+constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
+constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
+
+// Output channels are split over CS thread groups when a layer has fewer than 256 output pixels;
+// a group is 64 consecutive work items, i.e. one wave, so its channel offset is wave-uniform and the
+// weights come through scalar loads.
+constexpr int csplit(int npix, int cout) {
+    int c = 1;
+    while (npix * c < kThreads && c < cout) c *= 2;
+    return c;
+}
+
+// acc[k] = b[c0+k] + sum_ci,dy,dx w[c0+k][ci][dy][dx] in[ci][y+dy-1][x+dx-1]   (zero padding)
+template <int CIN, int CPT, int S>
+__device__ __forceinline__ void conv_pixel(const float* in, const float* __restrict__ w,
+                                           const float* __restrict__ b, int c0, int y, int x, float (&acc)[CPT]) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) acc[k] = b[c0 + k];
+#pragma unroll 2
+    for (int ci = 0; ci < CIN; ++ci) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+            const int yy = y + dy - 1;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                const int xx = x + dx - 1;
+                const float v = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
+#pragma unroll
+                for (int k = 0; k < CPT; ++k) acc[k] = fmaf(w[(((c0 + k) * CIN + ci) * 3 + dy) * 3 + dx], v, acc[k]);
+            }
+        }
+    }
+}
+
+// conv3x3 + bias + ReLU (+ MaxPool2d(2) when POOL, i.e. the pool that opens the next Down block):
+// in [CIN][S][S] -> out [COUT][S'][S'] (S' = S or S/2), LDS or global.
+template <int CIN, int COUT, int S, bool POOL>
+__device__ __forceinline__ void conv_layer(const float* in, float* out, const float* __restrict__ w,
+                                           const float* __restrict__ b, int tid) {
+    constexpr int SO = POOL ? S / 2 : S;
+    constexpr int NPIX = SO * SO;
+    constexpr int CS = csplit(NPIX, COUT), CPT = COUT / CS;
+    for (int it = tid; it < NPIX * CS; it += kThreads) {
+        const int grp = it / NPIX, p = it - grp * NPIX;
+        const int c0 = __builtin_amdgcn_readfirstlane(grp * CPT);
+        const int oy = p / SO, ox = p - oy * SO;
+        float res[CPT];
+        if constexpr (POOL) {
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) res[k] = 0.f;   // ReLU outputs are >= 0
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc[CPT];
+                conv_pixel<CIN, CPT, S>(in, w, b, c0, 2 * oy + (q >> 1), 2 * ox + (q & 1), acc);
+#pragma unroll
+                for (int k = 0; k < CPT; ++k) res[k] = fmaxf(res[k], acc[k]);
+            }
+        } else {
+            conv_pixel<CIN, CPT, S>(in, w, b, c0, oy, ox, res);
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) res[k] = fmaxf(res[k], 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * SO + ox] = res[k];
+    }
+}
+
+__device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, int kx) {
+    // otf: [65][128] half spectrum (kx-major); |H(ky,kx)|^2 for any kx via Hermitian symmetry
+    if (kx > 64) {
+        kx = 128 - kx;
+        ky = (128 - ky) & 127;
+    }
+    const float2 h = otf[kx * 128 + ky];
+    return h.x * h.x + h.y * h.y;
+}
+
+__global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __restrict__ otf128,
+                                                             const float* __restrict__ params,
+                                                             float* __restrict__ feat, int N) {
+    __shared__ __attribute__((aligned(16))) float A[kRegionA];
+    __shared__ __attribute__((aligned(16))) float B[kRegionB];
+    const int g = blockIdx.x;
+    if (g >= N) return;  // uniform per block; no barrier crossed
+    const int tid = threadIdx.x;
+    const float2* otf = otf128 + (size_t)g * 65 * 128;
+    // Down(1,4): MaxPool2d(2) of |H|^2 (128x128) -> A[64][64]; pooled[i][j] = max |H|^2 over
+    // rows ky = 2i, 2i+1 and columns kx = 2j, 2j+1.  Lanes take consecutive i (coalesced ky pairs).
+    for (int p = tid; p < 64 * 64; p += kThreads) {
+        const int j = p >> 6, i = p & 63;
+        const float m = fmaxf(fmaxf(mag2(otf, 2 * i, 2 * j), mag2(otf, 2 * i + 1, 2 * j)),
+                              fmaxf(mag2(otf, 2 * i, 2 * j + 1), mag2(otf, 2 * i + 1, 2 * j + 1)));
+        A[i * 64 + j] = m;
+    }
+    __syncthreads();
+    const float* P = params;
+#define GD_SN_LAYER(l, CI, CO, S, POOL, IN, OUT)                                                   \
+    conv_layer<CI, CO, S, POOL>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);           \
+    __syncthreads();
+    GD_SN_LAYER(0, 1, 4, 64, false, A, B)      // B[4][64][64]
+    GD_SN_LAYER(1, 4, 4, 64, true, B, A)       // A[4][32][32]   (+ MaxPool of Down(4,8))
+    GD_SN_LAYER(2, 4, 8, 32, false, A, B)      // B[8][32][32]
+    GD_SN_LAYER(3, 8, 8, 32, true, B, A)       // A[8][16][16]   (+ MaxPool of Down(8,16))
+    GD_SN_LAYER(4, 8, 16, 16, false, A, B)     // B[16][16][16]
+    GD_SN_LAYER(5, 16, 16, 16, true, B, A)     // A[16][8][8]    (+ MaxPool of Down(16,16))
+    GD_SN_LAYER(6, 16, 16, 8, false, A, B)     // B[16][8][8]
+#undef GD_SN_LAYER
+    // last conv of Down(16,16) straight to the feature vector [16][8][8]
+    conv_layer<16, 16, 8, false>(B, feat + (size_t)g * 1024, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+}
+
+}  // namespace subnet
+}  // namespace gd

@@ -38,6 +38,8 @@ SIGNATURES = {
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
     "gd_set_chunk_bytes": (_SZ, [_SZ]),
+    "gd_subnet_param_count": (_I, []),
+    "gd_subnet_features": (_I, [_P, _P, _P, _I, _P]),
     "gd_profile_enable": (_I, [_I]),
     "gd_profile_collect": (_I, []),
     "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),

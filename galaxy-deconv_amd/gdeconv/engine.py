@@ -159,6 +159,23 @@ def richardson_lucy(y, psf, n_iters):
     return out
 
 
+def subnet_features(otf128, params):
+    """SubNet conv features [N, 1024] from the 128x128 half-spectrum OTF of the PSFs
+    (``k_subnet_features``; ``params`` packed as documented in include/gdeconv.h)."""
+    _require_device(otf128, params)
+    lib = _lib.load()
+    N = otf128.shape[0]
+    if tuple(otf128.shape[1:]) != (65, 128) or otf128.dtype != torch.complex64:
+        raise ValueError("otf128 must be complex64 [N, 65, 128]")
+    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+        raise ValueError("bad SubNet parameter pack")
+    otf128 = otf128.contiguous()
+    feat = torch.empty(N, 1024, dtype=torch.float32, device=otf128.device)
+    _lib.check(lib.gd_subnet_features(otf128.data_ptr(), params.contiguous().data_ptr(), feat.data_ptr(), N,
+                                      _stream()), "gd_subnet_features")
+    return feat
+
+
 class ADMMState:
     """Device state of one unrolled-ADMM forward: the engine's opaque state buffer (OTF + u1 and
     v - u2, spectral for llh='Gaussian', spatial for 'Poisson') and ``zin``, the next denoiser
@@ -219,4 +236,4 @@ class ADMMState:
 
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
-           "ADMMState", "workspace", "empty_otf", "supported"]
+           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features"]

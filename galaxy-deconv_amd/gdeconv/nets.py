@@ -150,9 +150,32 @@ class SubNet(nn.Module):
         super().__init__()
         self.n = n
         self.conv_layers = nn.Sequential(_Down(1, 4), _Down(4, 8), _Down(8, 16), _Down(16, 16))
+        self.use_engine = True  # ROCm + eval: fused HIP feature extractor (gd_subnet_features)
         self.mlp = nn.Sequential(nn.Linear(16 * 8 * 8 + 1, 64), nn.ReLU(inplace=True),
                                  nn.Linear(64, 64), nn.ReLU(inplace=True),
                                  nn.Linear(64, 2 * n), nn.Softplus())
+
+    def _packed_params(self):
+        """Folded conv+BN weights of the 8 convs in gd_subnet_features order: per layer w then b."""
+        key = tuple(dc._fold_key() for dc in self._double_convs())
+        if getattr(self, "_pack", None) is None or self._pack[0] != key:
+            with torch.no_grad():
+                parts = []
+                for dc in self._double_convs():
+                    c1, b1, _, c2, b2, _ = dc.double_conv
+                    for conv, bn in ((c1, b1), (c2, b2)):
+                        w, b = _fold_conv_bn(conv, bn)
+                        parts += [w.reshape(-1), b.reshape(-1)]
+                self._pack = (key, torch.cat(parts).float().contiguous())
+        return self._pack[1]
+
+    def _double_convs(self):
+        return [down.maxpool_conv[1] for down in self.conv_layers]
+
+    def _engine_ok(self, kernel):
+        h, w = kernel.shape[-2:]
+        return (self.use_engine and kernel.is_cuda and not self.training and h == w and h % 2 == 0
+                and h <= 128 and all(dc.fold_bn for dc in self._double_convs()))
 
     def set_fold_bn(self, on):
         """Eval-mode BN folding (default on); off reproduces the reference's op order bit-exactly."""
@@ -163,11 +186,18 @@ class SubNet(nn.Module):
 
     def forward(self, kernel, alpha):
         N, _, h, w = kernel.shape
-        h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
-        w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2
-        k_pad = F.pad(kernel, (w1, w2, h1, h2), "constant", 0)
-        Hk = torch.fft.fftn(k_pad, dim=[2, 3])
-        feat = self.conv_layers((torch.abs(Hk) ** 2).float())
+        if self._engine_ok(kernel):
+            # HIP path: OTF at 128^2 (|.|^2 is shift invariant, so equal to |FFT2(pad128)|^2) and the
+            # fused conv stack k_subnet_features; the MLP below stays in PyTorch
+            from . import engine
+            otf128 = engine.psf_to_otf_half(kernel, N, 128, 128)
+            feat = engine.subnet_features(otf128, self._packed_params().to(kernel.device))
+        else:
+            h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
+            w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2
+            k_pad = F.pad(kernel, (w1, w2, h1, h2), "constant", 0)
+            Hk = torch.fft.fftn(k_pad, dim=[2, 3])
+            feat = self.conv_layers((torch.abs(Hk) ** 2).float())
         feat = torch.cat((feat.view(N, 1, 16 * 8 * 8), alpha.float().view(N, 1, 1)), dim=2)
         out = self.mlp(feat) + 1e-6
         rho1 = out[:, :, 0:self.n].view(N, 1, 1, self.n)

@@ -91,6 +91,15 @@ int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, in
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
 
+/* SubNet feature extractor (models/Unrolled_ADMM.py:77-84): from the 128x128 half-spectrum OTF
+ * of the PSFs (gd_psf_to_otf with H = W = 128; |OTF|^2 = |FFT2(pad128(psf))|^2), MaxPool2 and the
+ * four Down blocks' 8 conv3x3 + ReLU layers (BatchNorm folded in) -> feat [N][1024] in the
+ * reference's flatten order.  params: gd_subnet_param_count() floats, per conv layer l = 0..7
+ * (cin,cout) = (1,4),(4,4),(4,8),(8,8),(8,16),(16,16),(16,16),(16,16): weights [cout][cin][3][3]
+ * then bias [cout]. */
+int gd_subnet_param_count(void);
+int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream);
+
 /* Infinity-Cache chunking: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
  * run over the batch in chunks whose working set is about `bytes` (default 96 MiB), so spectra stay
  * resident in the 256 MiB Infinity Cache between kernels.  0 = whole batch per kernel.  Returns the

@@ -262,3 +262,29 @@ def test_full_size_conv_linearity_and_delta(eng, dev):
     delta[..., 24, 24] = 1.0                  # psf_to_otf maps pixel (h/2, h/2) to the origin
     ident = eng.conv_half(eng.psf_to_otf_half(delta, N, L, L), x)
     assert nerr(ident.cpu(), x.cpu()) < 2e-6
+
+
+# ------------------------------------------------------------------ SubNet feature kernel
+def test_subnet_feature_kernel_matches_pytorch(dev):
+    """k_subnet_features (|OTF_128|^2, pools, 8 folded conv+ReLU) vs the PyTorch SubNet layers in
+    the reference's op order, and the resulting rho1/rho2."""
+    from gdeconv import engine
+    from gdeconv.nets import SubNet
+    from gdeconv.synth import make_batch
+    from gdeconv.weights import make_state_dict
+    net = SubNet(8)
+    net.load_state_dict(make_state_dict(net, 11))
+    net = net.to(dev).eval()
+    _, psf, alpha, _ = make_batch(64, 64, seed=12)
+    psf, alpha = psf.to(dev), alpha.to(dev)
+    with torch.no_grad():
+        feat = engine.subnet_features(engine.psf_to_otf_half(psf, 64, 128, 128), net._packed_params().to(dev))
+        net.set_fold_bn(False)
+        kp = torch.nn.functional.pad(psf, (40, 40, 40, 40))
+        ref = net.conv_layers((torch.abs(torch.fft.fftn(kp, dim=[2, 3])) ** 2).float()).view(64, -1)
+        r1_ref, r2_ref = net(psf, alpha)           # PyTorch path (fold off -> engine path off)
+        net.set_fold_bn(True)
+        r1, r2 = net(psf, alpha)                   # engine path
+    assert nerr(feat.cpu(), ref.cpu()) < 1e-5
+    assert nerr(r1.reshape(64, -1).cpu(), r1_ref.reshape(64, -1).cpu()) < 1e-5
+    assert nerr(r2.reshape(64, -1).cpu(), r2_ref.reshape(64, -1).cpu()) < 1e-5

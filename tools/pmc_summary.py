@@ -21,6 +21,7 @@ MODE_NAMES = {
               "G_OTF_INIT", "G_INIT_W", "G_ITER"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
+    "k_subnet_features": ["FEATURES"],
 }
 
 
