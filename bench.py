@@ -29,9 +29,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s m
 
 # kernel mode ids (gd_engine.hip enums) -> readable names
 MODE_NAMES = {
-    "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO"],
+    "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO", "YA"],
     "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV",
-              "G_OTF_INIT", "G_INIT_W", "G_ITER"],
+              "G_INIT", "G_ITER", "G_ITER0"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES"],
@@ -41,7 +41,19 @@ MODE_NAMES = {
 def pretty(name):
     k, rest = name.split("<")
     L, mode = rest.rstrip(">").split(",")
+    if k.startswith("op_"):
+        return f"{k}<{L},{['Gaussian', 'Poisson'][int(mode)]}>"
     return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
+
+
+def op_bytes(name, L, n_iters):
+    """Algorithmic bytes per galaxy of one whole engine operation (its kernels' compulsory traffic):
+    Gaussian ADMM iteration = RF(z) + C_G_ITER + RI(zin), averaged over first / middle / last."""
+    img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
+    if pretty(name) == f"op_admm_iter<{L},Gaussian>":
+        c = (6.5 + 7.5 * max(0, n - 2) + 4.5 * (n > 1)) / n
+        return 2 * img + (2 + c) * half
+    return None
 
 
 def kernel_bytes(name, L, n_iters):
@@ -53,12 +65,13 @@ def kernel_bytes(name, L, n_iters):
     n = max(1, n_iters)
     k = pretty(name)
     table = {
-        # Gaussian (spectral state): RF(z) -> C_G_ITER -> RI(zin)
+        # Gaussian (spectral state |H|^2, G = conj(H)F(y/a), U1, W~ = conj(H)W): RF(z) -> C_G_ITER -> RI(zin)
         f"k_row_fwd<{L},ONE>": img + half,                                  # z -> T
-        f"k_col<{L},G_ITER>": half * (7 + 8 * max(0, n - 2) + 4 * (n > 1)) / n,  # T,H,U1,W,F(y/a) -> U1,W,T
+        f"k_col<{L},G_ITER>": half * (7.5 * max(0, n - 2) + 4.5 * (n > 1)) / max(1, n - 1),  # T,|H|^2,G,U1,W~ -> U1,W~,T
+        f"k_col<{L},G_ITER0>": half * 6.5,                                  # T, x0 T, |H|^2, G -> U1, W~, T
         f"k_row_inv<{L},OUT1>": half + img,                                 # T -> zin | x
-        f"k_col<{L},G_OTF_INIT>": 2 * half + 3 * half,                      # T(2) -> OTF, F(y/a), T
-        f"k_col<{L},G_INIT_W>": 3 * half + half,                            # T, OTF, F(y/a) -> W
+        f"k_row_fwd<{L},YA>": img + half,                                   # y -> T
+        f"k_col<{L},G_INIT>": half + 2.5 * half,                            # T -> |H|^2, G, T (PSF: 9 KB)
         # Poisson (spatial u1, w): RF(z-u1, w) -> C_ITER -> RI_ITER
         f"k_row_fwd<{L},ITER>": 3 * img + 2 * half,
         f"k_col<{L},ITER>": 5 * half,
@@ -94,6 +107,7 @@ def parse():
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--chunk-mb", type=float, default=None,
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
+    p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
     return p.parse_args()
@@ -150,6 +164,9 @@ def main():
         lib.gd_set_chunk_bytes(int(args.chunk_mb * (1 << 20)))
     chunk_bytes = lib.gd_set_chunk_bytes(0)
     lib.gd_set_chunk_bytes(chunk_bytes)
+    if args.pipe_streams is not None:
+        lib.gd_set_pipeline_streams(args.pipe_streams)
+    pipe_streams = lib.gd_set_pipeline_streams(0)
 
     N, L, n = args.batch, args.size, args.n_iters
     obs, psf, alpha, _ = make_batch(N, L, seed=20250307 + rank, device=dev)
@@ -167,7 +184,8 @@ def main():
         if world > 1:
             dist.barrier()
         _lib.profile_reset()
-        _lib.profile_enable(True)
+        # pipelined chunks: time whole operations only (per-launch events would perturb them)
+        _lib.profile_enable(1 if chunk_bytes > 0 else 2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -176,7 +194,7 @@ def main():
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
-        _lib.profile_enable(False)
+        _lib.profile_enable(0)
         kstats = _lib.profile_collect()
         assert torch.isfinite(out).all(), "non-finite output"
 
@@ -196,18 +214,30 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
-    # per-kernel live timing (HIP events on the engine's launch stream over the timed region)
+    # live timing: HIP events recorded by the library on each kernel's launch stream and, for whole
+    # operations (op_*), on the caller's stream, over the timed region
     kernels = {pretty(k): {"avg_ms": ms / c, "launches": c} for k, (ms, c) in kstats.items()}
-    dom_raw = max(kstats, key=lambda k: kstats[k][0])
-    dom_ms = kstats[dom_raw][0] / kstats[dom_raw][1]
-    per_gal = kernel_bytes(dom_raw, L, n)
+    ops = {k: v for k, v in kstats.items() if k.startswith("op_")}
+    kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
+    pipelined = chunk_bytes > 0
+    if pipelined and ops and not kern:
+        # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
+        # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
+        dom_raw = max(ops, key=lambda k: ops[k][0])
+        dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
+        per_gal = op_bytes(dom_raw, L, n)
+    else:
+        dom_raw = max(kern, key=lambda k: kern[k][0])
+        dom_ms = kern[dom_raw][0] / kern[dom_raw][1]
+        per_gal = kernel_bytes(dom_raw, L, n)
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
         ent = tj.get("kernels", {}).get(pretty(dom_raw))
-        if ent and tj.get("batch") == N and tj.get("size") == L:
+        same_engine = tj.get("engine_rev") == lib.gd_engine_rev().decode()
+        if ent and same_engine and tj.get("batch") == N and tj.get("size") == L:
             traffic = ent.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -228,7 +258,7 @@ def main():
                                f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])",
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
                    "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
-                   "chunk_mib": chunk_bytes / (1 << 20)},
+                   "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1},
         "roofline": roofline,
         "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},

@@ -69,14 +69,18 @@ struct Args {
     int llh;               // GD_LLH_GAUSSIAN / GD_LLH_POISSON
     int last;              // final ADMM iteration: write x (times alpha for Poisson)
     int first;             // first ADMM iteration: spectral u1 is zero (not read)
-    float2* s_yal;         // Gaussian spectral state [N][K][L]: F(max(y,0)/alpha)
-    float2* s_u1;          //                                     F(u1)
-    float2* s_w;           //                                     F(v - u2)
+    float* s_hh;           // Gaussian spectral state [N][K][L]: |H|^2
+    float2* s_g;           //   conj(H) F(max(y,0)/alpha)
+    float2* s_u1;          //   F(u1)
+    float2* s_w;           //   conj(H) F(v - u2)
+    int t_slot;            // image slot of T that row-forward kernels write (RIF_CLAMP -> 1)
+    float2* Tw;            // if set: row-forward kernels write here (full-batch layout) instead of T
+    float2* Tx0;           // Gaussian iteration 0: x0's row spectra (slot 1, full-batch layout)
 };
 
-enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO };
+enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA };
 enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV,
-               C_G_OTF_INIT, C_G_INIT_W, C_G_ITER };
+               C_G_INIT, C_G_ITER, C_G_ITER0 };
 enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
 enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
@@ -95,8 +99,6 @@ struct Geo {
     static constexpr int RB = rows_per_block(LPB, L);  // rows per row-kernel block (even, divides L)
     static constexpr int RLD = L + 2;                  // row buffer leading dim (bank spread)
     static constexpr int XCH = xch_elems<L>();
-    // row kernels (at most LPB lines): row buffer | exchange areas | staged / result images
-    static constexpr int ROW_LDS = cmax(cmax(LPB * RLD, LPB * XCH), LPB * L);
     static constexpr int COL_LDS = LPB * XCH;
     static_assert(L % RB == 0 && RB % 2 == 0, "rows per block must be even and divide L");
 };
@@ -128,44 +130,45 @@ __device__ __forceinline__ float v_step(int llh, float vt, float yp, float rho2,
 // row 2m+1 -> imaginary part).  Packing two different images instead would extract the smaller
 // one's spectrum from the rounding noise of the larger (a PSF of sum 1/16 next to an observation of
 // ~1e2 ADU loses every digit), while rows of one image share its scale exactly as a 2D FFT does.
-template <int L, int NI>
+template <int L, int NI, int RBX = 0>
 struct RowGeo {
     using G = Geo<L>;
-    // rows per block, per image (even, divides L): up to LPB lines (256 threads) per block, so a
-    // single-image kernel takes twice the rows of a two-image one
-    static constexpr int RB = rows_per_block(2 * G::LPB / NI, L);
+    // rows per block, per image (even, divides L): by default up to LPB lines (256 threads) per
+    // block, so a single-image kernel takes twice the rows of a two-image one; RBX overrides
+    static constexpr int RB = RBX ? RBX : rows_per_block(2 * G::LPB / NI, L);
     static constexpr int PAIRS = RB / 2;    // lines per image
     static constexpr int LINES = NI * PAIRS;
     static constexpr int THREADS = LINES * G::F1;
-    static_assert(RB % 2 == 0, "row pairs");
+    // LDS (float2): row buffer | per-line exchange areas | staged input / result rows, aliased
+    static constexpr int LDS = cmax(cmax(LINES * G::RLD, LINES * G::XCH), (NI * RB * L + 1) / 2);
+    static_assert(RB % 2 == 0 && L % RB == 0, "row pairs must tile the image");
+    static_assert(THREADS <= 1024, "block too large");
 };
 
 // Split line spectra C = FFT(row_even + i row_odd) (row buffer [line][k]) into the two rows'
 // half spectra, stored transposed T[g][im][k][row0 + rr]; consecutive threads take consecutive rows.
-template <int L, int NI>
+template <int L, typename R>
 __device__ __forceinline__ void split_store(const Args& a, const float2* rowbuf, int g, int row0, int tid) {
     using G = Geo<L>;
-    using R = RowGeo<L, NI>;
-    for (int idx = tid; idx < NI * G::K * R::RB; idx += R::THREADS) {
-        const int rr = idx % R::RB, t = idx / R::RB;
+    for (int idx = tid; idx < R::LINES * G::K; idx += R::THREADS) {
+        const int m = idx % R::PAIRS, t = idx / R::PAIRS;
         const int k = t % G::K, im = t / G::K;
-        const int line = im * R::PAIRS + (rr >> 1);
+        const int line = im * R::PAIRS + m;
         const float2 C = rowbuf[line * G::RLD + k];
         const float2 D = rowbuf[line * G::RLD + (k == 0 ? 0 : L - k)];
-        const float2 o = (rr & 1) ? make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x))   // (C - conj D)/(2i)
-                                  : make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));  // (C + conj D)/2
-        a.T[tidx(g, im, k, row0 + rr, G::K, L)] = o;
+        // row 2m: (C + conj D)/2 ; row 2m+1: (C - conj D)/(2i) -> adjacent in T: one 16-byte store
+        *reinterpret_cast<float4*>((a.Tw ? a.Tw : a.T) + tidx(g, im + a.t_slot, k, row0 + 2 * m, G::K, L)) =
+            make_float4(0.5f * (C.x + D.x), 0.5f * (C.y - D.y), 0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
     }
 }
 
 // Gather the half spectra of rows 2m, 2m+1 of each image into the Hermitian-extended packed line
 // spectrum D = R_even + i R_odd over kx in [0, L) (row buffer [line][k]).  One 16-byte load per
 // (image, k, pair): the two rows are adjacent in the transposed layout.
-template <int L, int NI>
+template <int L, typename R>
 __device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g, int row0, int tid) {
     using G = Geo<L>;
-    using R = RowGeo<L, NI>;
-    for (int idx = tid; idx < NI * G::K * R::PAIRS; idx += R::THREADS) {
+    for (int idx = tid; idx < R::LINES * G::K; idx += R::THREADS) {
         const int m = idx % R::PAIRS, t = idx / R::PAIRS;
         const int k = t % G::K, im = t / G::K;
         const float4 q = *reinterpret_cast<const float4*>(a.T + tidx(g, im, k, row0 + 2 * m, G::K, L));
@@ -184,7 +187,7 @@ __device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g
 // ---------------------------------------------------------------- RF: row forward
 template <int MODE>
 struct RfTraits {
-    static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE) ? 1 : 2;
+    static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE || MODE == RF_YA) ? 1 : 2;
 };
 
 // Four consecutive pixels of image `im` starting at flat pixel index `pix` (row-major, 16-byte
@@ -220,19 +223,23 @@ __device__ __forceinline__ float4 rf_source4(const Args& a, int g, int im, int r
         }
     } else if constexpr (MODE == RF_ONE) {
         return ld4(a.a0 + pix);
+    } else if constexpr (MODE == RF_YA) {
+        const float4 y = ld4(a.y + pix);
+        const float al = a.alpha(g);                                   // max(y,0) / alpha
+        return make_float4(fmaxf(y.x, 0.f) / al, fmaxf(y.y, 0.f) / al, fmaxf(y.z, 0.f) / al, fmaxf(y.w, 0.f) / al);
     } else {
         return ld4((im == 0 ? a.a0 : a.a1) + pix);
     }
 }
 
-template <int L, int MODE>
-__global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI>::THREADS)) void k_row_fwd(Args a) {
+template <int L, int MODE, int RBX = 0>
+__global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI, RBX>::THREADS)) void k_row_fwd(Args a) {
     constexpr int NI = RfTraits<MODE>::NI;
     using G = Geo<L>;
-    using R = RowGeo<L, NI>;
+    using R = RowGeo<L, NI, RBX>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[R::LDS];
     const int tid = threadIdx.x;
     const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
@@ -261,20 +268,18 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI>::THREADS)) void k_ro
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
-    split_store<L, NI>(a, lds, g, row0, tid);
+    split_store<L, R>(a, lds, g, row0, tid);
 }
 
 // ---------------------------------------------------------------- C: column pass
 template <int MODE>
 struct ColTraits {
     static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
-                                 MODE == C_WIENER || MODE == C_CONV2 || MODE == C_G_OTF_INIT);
+                                 MODE == C_WIENER || MODE == C_CONV2);
     static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
-    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_INIT_W);
-    static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF ||
-                                       MODE == C_G_OTF_INIT);
-    static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2 ||
-                                      MODE == C_G_INIT_W || MODE == C_G_ITER);
+    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD);
+    static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
+    static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2);
     static constexpr bool FWD = (MODE != C_INV);
 };
 
@@ -303,12 +308,17 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         P[s] = a.T[c0 + j + F1 * s];
         if constexpr (TR::IN2) Q[s] = a.T[c1 + j + F1 * s];
     }
+    constexpr bool gfirst = (MODE == C_G_ITER0);  // iteration 0: x0's row spectra wait in Tx0 slot 1
+    if constexpr (gfirst) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) Q[s] = a.Tx0[c1 + j + F1 * s];
+    }
     float2 Hpre[VAR == 2 ? F2 : 1], Wpre[VAR == 2 ? F2 : 1];
     if constexpr (VAR == 2 && MODE == C_G_ITER) {
         const size_t ob0 = ((size_t)g * K + kx) * L;
 #pragma unroll
         for (int s = 0; s < F2; ++s) {
-            Hpre[s] = a.otf[ob0 + j + F1 * s];
+            Hpre[s] = make_float2(0.f, 0.f);
             Wpre[s] = a.s_w[ob0 + j + F1 * s];
         }
     }
@@ -316,20 +326,72 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     if constexpr (TR::FWD && VAR != 1) {
         line_fft<L, false>(P, j, my, tw);
         if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
+        if constexpr (gfirst) line_fft<L, false>(Q, j, my, tw);
+    }
+    // C_G_INIT: the OTF column H(., kx) straight from the h x h PSF: row DFT at kx of the (at most h)
+    // non-zero rows of the circularly shifted, zero-padded PSF, then the column FFT.  The PSFs of the
+    // (at most two) galaxies this block touches are staged in LDS (rows padded to h+1).
+    float2 Hc[MODE == C_G_INIT ? F2 : 1];
+    if constexpr (MODE == C_G_INIT) {
+        const int h = a.h, hp = h + 1, c0p = h >> 1;
+        constexpr int NGB = (G::LPB + K - 2) / K + 1;                  // galaxies a block can touch
+        const int gb = (blockIdx.x * G::LPB) / K;                      // first galaxy of the block
+        const bool staged = NGB * h * hp <= G::COL_LDS * 2;
+        float* pl = reinterpret_cast<float*>(xch);
+        if (staged) {
+            __syncthreads();  // (the forward FFT above used xch)
+            const int ng = (a.N - gb < NGB) ? a.N - gb : NGB;
+            for (int q = tid; q < ng * h * h; q += 256) {
+                const int gg = q / (h * h), rem = q - gg * h * h, i = rem / h, jj = rem - i * h;
+                pl[(gg * h + i) * hp + jj] = a.psf[(long long)(gb + gg) * a.psf_gstride + rem];
+            }
+            __syncthreads();
+        }
+        const float* ps = staged ? pl + (g - gb) * h * hp : a.psf + (long long)g * a.psf_gstride;
+        const int ld = staged ? hp : h;
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            int i = j + F1 * s + c0p;
+            if (i >= L) i -= L;
+            float2 acc0 = make_float2(0.f, 0.f), acc1 = acc0;
+            if (i < h) {
+                const float* row = ps + i * ld;
+                int c = (L - c0p) % L;                 // column offset of jj = 0
+                int jj = 0;
+                for (; jj + 1 < h; jj += 2) {           // two independent accumulators
+                    const int c1 = (c + 1 == L) ? 0 : c + 1;
+                    const float2 w0 = tw[(kx * c) % L], w1 = tw[(kx * c1) % L];
+                    const float v0 = row[jj], v1 = row[jj + 1];
+                    acc0.x = fmaf(v0, w0.x, acc0.x);
+                    acc0.y = fmaf(v0, w0.y, acc0.y);
+                    acc1.x = fmaf(v1, w1.x, acc1.x);
+                    acc1.y = fmaf(v1, w1.y, acc1.y);
+                    c = (c1 + 1 == L) ? 0 : c1 + 1;
+                }
+                if (jj < h) {
+                    const float2 w0 = tw[(kx * c) % L];
+                    acc0.x = fmaf(row[jj], w0.x, acc0.x);
+                    acc0.y = fmaf(row[jj], w0.y, acc0.y);
+                }
+            }
+            Hc[s] = cadd(acc0, acc1);
+        }
+        if (staged) __syncthreads();  // PSF staging area -> exchange areas
+        line_fft<L, false>(Hc, j, my, tw);
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
-    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_OTF_INIT) ? a.alpha(g) : 1.f;
-    const float r1 = (MODE == C_ITER || MODE == C_G_ITER) ? a.rho1(g) : 0.f;
-    const float r2 = (MODE == C_ITER || MODE == C_G_ITER) ? a.rho2(g) : 0.f;
-    const bool glast = (MODE == C_G_ITER) && a.last;
-    const float r2n = (MODE == C_G_INIT_W || (MODE == C_G_ITER && !glast)) ? a.rho2n(g) : 0.f;
+    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_INIT) ? a.alpha(g) : 1.f;
+    constexpr bool giter = (MODE == C_G_ITER || MODE == C_G_ITER0);
+    const float r1 = (MODE == C_ITER || giter) ? a.rho1(g) : 0.f;
+    const float r2 = (MODE == C_ITER || giter) ? a.rho2(g) : 0.f;
+    const bool glast = giter && a.last;
+    const float r2n = (giter && !glast) ? a.rho2n(g) : 0.f;
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
         float2 Hk = make_float2(0.f, 0.f);
-        if constexpr (VAR == 2 && MODE == C_G_ITER) Hk = Hpre[s];
-        else if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
+        if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
         if constexpr (TR::STORE_OTF || MODE == C_WIENER) Hk = P[s];
         if constexpr (TR::STORE_OTF) {
             if (valid) a.otf[ob + ky] = Hk;
@@ -350,49 +412,54 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float lhs = HtH + 1.0f / al;
             const float2 rhs = cmulc(Q[s], Hk);
             P[s] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
-        } else if constexpr (MODE == C_G_OTF_INIT) {
-            // as C_OTF_INIT, and keep F(y/alpha) as Gaussian spectral state
-            if (valid) a.s_yal[ob + ky] = Q[s];
-            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
-            const float lhs = HtH + 1.0f / al;
-            const float2 rhs = cmulc(Q[s], Hk);
-            P[s] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
-        } else if constexpr (MODE == C_G_INIT_W) {
-            // first V step in the spectral domain (u1 = u2 = 0): W1 = V1 = (rho2 (H X0 + 0) + F(y/alpha)) / (1 + rho2)
-            const float2 HX = cmul(Hk, P[s]);
-            const float2 Ya = a.s_yal[ob + ky];
-            const float d = 1.0f + r2n;
-            if (valid) a.s_w[ob + ky] = make_float2((r2n * HX.x + Ya.x) / d, (r2n * HX.y + Ya.y) / d);
-        } else if constexpr (MODE == C_G_ITER) {
-            // Gaussian ADMM iteration entirely in the spectral domain (all steps of
-            // models/Unrolled_ADMM.py:207-213 are linear for llh='Gaussian'):
-            //   X   = (rho1 (Z - U1) + rho2 conj(H) W) / (rho1 |H|^2 + rho2)      runtime X_Update :315-319
-            //   U1' = (U1 + X) - Z ;  U2' = H X - W                               :212-213 (W = V - U2)
-            //   V'  = (rho2' (H X + U2') + F(y/alpha)) / (1 + rho2') ;  W' = V' - U2'   V step :335-336
-            //   out = X + U1' (next denoiser input)  |  X (last iteration)
+        } else if constexpr (MODE == C_G_INIT) {
+            // init_l2 (models/Unrolled_ADMM.py:170-175) and the Gaussian constants:
+            //   |H|^2, G = conj(H) F(y/alpha) kept as state;  X0 = G / (|H|^2 + 1/alpha)
+            const float2 Hk2 = Hc[s];
+            const float hh = Hk2.x * Hk2.x + Hk2.y * Hk2.y;
+            const float2 Gk = cmulc(P[s], Hk2);
+            if (valid) {
+                a.s_hh[ob + ky] = hh;
+                a.s_g[ob + ky] = Gk;
+            }
+            const float lhs = hh + 1.0f / al;
+            P[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+        } else if constexpr (giter) {
+            // Gaussian ADMM iteration entirely in the spectral domain (every step of
+            // models/Unrolled_ADMM.py:207-213 is linear for llh='Gaussian'), with the v - u2 state
+            // kept premultiplied by conj(H) (W~ = conj(H) W) so only |H|^2 and G are needed:
+            //   X    = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2 + rho2)        X_Update :315-319
+            //   U1'  = (U1 + X) - Z                                            :212
+            //   U2~  = |H|^2 X - W~                     (= conj(H) (H X - W))   :213
+            //   V~   = (rho2' (|H|^2 X + U2~) + G) / (1 + rho2')               V step :335-336
+            //   W~'  = V~ - U2~ ;  out = X + U1' (next denoiser input) | X (last iteration)
+            // First iteration: U1 = 0 and W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2).
             const float2 Zk = P[s];
-            const float2 U1 = a.first ? make_float2(0.f, 0.f) : a.s_u1[ob + ky];
-            float2 Wk;
-            if constexpr (VAR == 2) Wk = Wpre[s];
-            else Wk = a.s_w[ob + ky];
-            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
-            const float lhs = r1 * HtH + r2;
+            const float hh = a.s_hh[ob + ky];
+            float2 U1 = make_float2(0.f, 0.f), Wt, Gk = make_float2(0.f, 0.f);
+            if (gfirst || !glast) Gk = a.s_g[ob + ky];
+            if constexpr (gfirst) {
+                const float d0 = 1.0f + r2;
+                Wt = make_float2((r2 * (hh * Q[s].x + 0.0f) + Gk.x) / d0, (r2 * (hh * Q[s].y + 0.0f) + Gk.y) / d0);
+            } else {
+                U1 = a.s_u1[ob + ky];
+                if constexpr (VAR == 2) Wt = Wpre[s];
+                else Wt = a.s_w[ob + ky];
+            }
+            const float lhs = r1 * hh + r2;
             const float2 A = csub(Zk, U1);
-            const float2 HtW = cmulc(Wk, Hk);
-            const float2 rhs = make_float2(r1 * A.x + r2 * HtW.x, r1 * A.y + r2 * HtW.y);
-            const float2 X = make_float2(rhs.x / lhs, rhs.y / lhs);
+            const float2 X = make_float2((r1 * A.x + r2 * Wt.x) / lhs, (r1 * A.y + r2 * Wt.y) / lhs);
             if (glast) {
                 P[s] = cscale(X, inv_n);
             } else {
                 const float2 U1n = csub(cadd(U1, X), Zk);
-                const float2 HX = cmul(Hk, X);
-                const float2 U2n = csub(HX, Wk);
-                const float2 Ya = a.s_yal[ob + ky];
+                const float2 HHX = cscale(X, hh);
+                const float2 U2t = csub(HHX, Wt);
                 const float d = 1.0f + r2n;
-                const float2 Vn = make_float2((r2n * (HX.x + U2n.x) + Ya.x) / d, (r2n * (HX.y + U2n.y) + Ya.y) / d);
+                const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
                 if (valid) {
                     a.s_u1[ob + ky] = U1n;
-                    a.s_w[ob + ky] = csub(Vn, U2n);
+                    a.s_w[ob + ky] = csub(Vt, U2t);
                 }
                 P[s] = cscale(cadd(X, U1n), inv_n);
             }
@@ -439,14 +506,14 @@ struct RiTraits {
     static constexpr int NI = (MODE == RI_ITER || MODE == RI_OUT2) ? 2 : 1;
 };
 
-template <int L, int MODE>
-__global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI>::THREADS)) void k_row_inv(Args a) {
+template <int L, int MODE, int RBX = 0>
+__global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI, RBX>::THREADS)) void k_row_inv(Args a) {
     constexpr int NI = RiTraits<MODE>::NI;
     using G = Geo<L>;
-    using R = RowGeo<L, NI>;
+    using R = RowGeo<L, NI, RBX>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[R::LDS];
     const int tid = threadIdx.x;
     const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
@@ -454,7 +521,7 @@ __global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI>::THREADS)) void k_ro
     const int line = tid / F1, j = tid - line * F1;
     const int im = line / R::PAIRS, m = line - im * R::PAIRS;
     fill_twiddles<L>(tw, tid, R::THREADS);
-    gather_rows<L, NI>(a, lds, g, row0, tid);
+    gather_rows<L, R>(a, lds, g, row0, tid);
     __syncthreads();
     float2 v[F2];
 #pragma unroll
@@ -547,13 +614,13 @@ __device__ __forceinline__ float rif_point(const Args& a, int g, int r, int c, f
     }
 }
 
-template <int L, int MODE>
-__global__ __launch_bounds__((RowGeo<L, 1>::THREADS)) void k_row_invfwd(Args a) {
+template <int L, int MODE, int RBX = 0>
+__global__ __launch_bounds__((RowGeo<L, 1, RBX>::THREADS)) void k_row_invfwd(Args a) {
     using G = Geo<L>;
-    using R = RowGeo<L, 1>;
+    using R = RowGeo<L, 1, RBX>;
     constexpr int F1 = G::F1, F2 = G::F2;
     __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 lds[G::ROW_LDS];
+    __shared__ __attribute__((aligned(16))) float2 lds[R::LDS];
     const int tid = threadIdx.x;
     const int blocks_per_g = L / R::RB;
     const int g = blockIdx.x / blocks_per_g;
@@ -561,7 +628,7 @@ __global__ __launch_bounds__((RowGeo<L, 1>::THREADS)) void k_row_invfwd(Args a) 
     const int line = tid / F1, j = tid - line * F1;
     const int rA = row0 + 2 * line;
     fill_twiddles<L>(tw, tid, R::THREADS);
-    gather_rows<L, 1>(a, lds, g, row0, tid);
+    gather_rows<L, R>(a, lds, g, row0, tid);
     __syncthreads();
     float2 v[F2];
 #pragma unroll
@@ -581,7 +648,7 @@ __global__ __launch_bounds__((RowGeo<L, 1>::THREADS)) void k_row_invfwd(Args a) 
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
-    split_store<L, 1>(a, lds, g, row0, tid);
+    split_store<L, R>(a, lds, g, row0, tid);
 }
 
 // ---------------------------------------------------------------- host-side launch helpers
@@ -618,7 +685,7 @@ struct ProfStat {
     long long launches = 0;
 };
 std::mutex g_prof_mu;
-bool g_prof_on = false;
+int g_prof_level = 0;  // 0 off, 1 whole operations (op_*), 2 operations + every kernel launch
 std::vector<ProfEntry> g_prof_pending;
 std::vector<hipEvent_t> g_prof_pool;
 std::map<std::string, ProfStat> g_prof_stats;
@@ -638,9 +705,9 @@ struct ProfScope {
     bool on;
     ProfEntry ent;
     hipStream_t st;
-    ProfScope(const std::string& name, hipStream_t s) : on(false), st(s) {
+    ProfScope(const std::string& name, hipStream_t s, int level = 2) : on(false), st(s) {
         std::lock_guard<std::mutex> lk(g_prof_mu);
-        if (!g_prof_on) return;
+        if (g_prof_level < level) return;
         on = true;
         ent.name = name;
         ent.start = prof_event();
@@ -697,12 +764,42 @@ struct Launcher {
         if (_rc != GD_OK) return _rc; \
     } while (0)
 
-// ---------------------------------------------------------------- Infinity-Cache chunking
-// A multi-kernel operation runs chunk by chunk over the batch: each chunk's spectral workspace
-// (and the images the row passes read twice) stays resident in the 256 MiB Infinity Cache between
-// its kernels instead of round-tripping through HBM.  g_chunk_bytes is the target resident working
-// set per chunk (0 = whole batch in one pass).
-size_t g_chunk_bytes = 0;  // measured: chunking slower at 256^2 (small-grid fill/drain > MALL gain)
+// ---------------------------------------------------------------- Infinity-Cache pipelining
+// A multi-kernel operation runs over the batch in chunks of G galaxies; consecutive chunks go to
+// g_pipe_streams internal HIP streams, forked from and joined back into the caller's stream with
+// events (the call stays ordered on - and graph-capturable through - the caller's stream).  Each
+// internal stream owns a region of the workspace, so a chunk's spectra stay resident in the 256 MiB
+// Infinity Cache between its kernels while the other streams keep the chip full (measured at 256^2:
+// one ADMM iteration 7-11 % faster than one pass over the batch; plain sequential chunks on one
+// stream were slower than one pass because small grids fill and drain).
+size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk; 0 = one pass
+int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
+constexpr int kMaxPipe = 8;
+
+struct PipeRes {
+    bool ok = false;
+    hipStream_t st[kMaxPipe];
+    hipEvent_t fork;
+    hipEvent_t join[kMaxPipe];
+};
+PipeRes g_pipe[64];
+std::mutex g_pipe_mu;
+
+inline PipeRes* pipe_res() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    PipeRes& r = g_pipe[dev];
+    if (!r.ok) {
+        for (int i = 0; i < kMaxPipe; ++i) {
+            if (hipStreamCreateWithFlags(&r.st[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
+            if (hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+        }
+        if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+        r.ok = true;
+    }
+    return &r;
+}
 
 inline Args offset_args(const Args& a, int g0, int n, int L) {
     Args b = a;
@@ -710,9 +807,12 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
     const size_t img = (size_t)g0 * L * L;
     const size_t spec = (size_t)g0 * (L / 2 + 1) * L;
     if (b.otf) b.otf += spec;
-    if (b.s_yal) b.s_yal += spec;
+    if (b.s_hh) b.s_hh += spec;
+    if (b.s_g) b.s_g += spec;
     if (b.s_u1) b.s_u1 += spec;
     if (b.s_w) b.s_w += spec;
+    if (b.Tw) b.Tw += 2 * spec;   // full-batch workspace layouts [N][2][K][L]
+    if (b.Tx0) b.Tx0 += 2 * spec;
     if (b.y) b.y += img;
     if (b.a0) b.a0 += img;
     if (b.a1) b.a1 += img;
@@ -724,21 +824,42 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
     GalScalar* gs[] = {&b.alpha, &b.rho1, &b.rho2, &b.rho2n};
     for (GalScalar* x : gs)
         if (x->p) x->p += (long long)g0 * x->stride;
-    return b;  // T (workspace) is not offset: every chunk reuses its head
+    return b;  // T is set per chunk to its stream's workspace region
 }
 
+// f(const Args& chunk, hipStream_t stream) enqueues one chunk's kernels on `stream`.
 template <typename F>
-int for_chunks(const Args& a, int L, size_t per_galaxy_bytes, F&& f) {
+int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
+    const size_t tgal = (size_t)2 * (L / 2 + 1) * L * sizeof(float2);  // workspace per galaxy
     int G = a.N;
-    if (g_chunk_bytes && per_galaxy_bytes) {
-        const size_t g = g_chunk_bytes / per_galaxy_bytes;
+    if (g_chunk_bytes) {
+        const size_t g = g_chunk_bytes / tgal;
         G = (int)(g < 1 ? 1 : (g > (size_t)a.N ? (size_t)a.N : g));
     }
-    for (int g0 = 0; g0 < a.N; g0 += G) {
-        const int n = (a.N - g0 < G) ? a.N - g0 : G;
-        GD_TRY(f(offset_args(a, g0, n, L)));
+    if (G >= a.N) return f(a, st);
+    int S = g_pipe_streams < kMaxPipe ? g_pipe_streams : kMaxPipe;
+    if (S > a.N / G) S = a.N / G;  // regions must fit the caller's workspace
+    PipeRes* r = S > 1 ? pipe_res() : nullptr;
+    if (!r) S = 1;
+    if (S > 1) {
+        if (hipEventRecord(r->fork, st) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
+        for (int i = 0; i < S; ++i)
+            if (hipStreamWaitEvent(r->st[i], r->fork, 0) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
     }
-    return GD_OK;
+    int rc = GD_OK;
+    for (int g0 = 0, c = 0; g0 < a.N && rc == GD_OK; g0 += G, ++c) {
+        const int n = (a.N - g0 < G) ? a.N - g0 : G;
+        Args b = offset_args(a, g0, n, L);
+        b.T = a.T + (size_t)(c % S) * G * 2 * (L / 2 + 1) * L;
+        rc = f(b, S > 1 ? r->st[c % S] : st);
+    }
+    if (S > 1) {
+        for (int i = 0; i < S; ++i) {
+            if (hipEventRecord(r->join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(st, r->join[i], 0) != hipSuccess)
+                return fail(GD_ERR_HIP, "pipeline join");
+        }
+    }
+    return rc;
 }
 
 // Operation bodies, templated on L.
@@ -763,9 +884,9 @@ struct Ops {
         GD_TRY(Lc::template col<C_INV>(a, st));
         return Lc::template ri<RI_OUT1>(a, st);
     }
-    static int admm_init(Args a0, hipStream_t st) {
-        // a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
-        return for_chunks(a0, L, 2 * HALF + 4 * IMG, [&](const Args& a) {
+    static int admm_init(Args a0, hipStream_t st0) {
+        // Poisson: a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
             GD_TRY(Lc::template col<C_OTF_INIT>(b, st));
@@ -775,44 +896,51 @@ struct Ops {
             return Lc::template ri<RI_INIT>(a, st);
         });
     }
-    static int admm_init_gauss(Args a0, hipStream_t st) {
-        // spectral state: otf, s_yal, s_w (s_u1 implicitly 0); a.o2 = zin (x0)
-        return for_chunks(a0, L, 2 * HALF + 4 * IMG, [&](const Args& a) {
+    static int admm_init_gauss(Args a0, hipStream_t st0) {
+        // Gaussian state |H|^2, G; x0 -> zin (a.o2); x0's row spectra -> slot 1 of the FULL workspace
+        // where iteration 0 picks them up (Tx0), whatever the chunking
+        a0.Tw = nullptr;
+        a0.Tx0 = a0.T;  // full-batch workspace, offset per chunk
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
-            GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
-            GD_TRY(Lc::template col<C_G_OTF_INIT>(b, st));
-            b.o0 = a.o2;  // RIF_CLAMP writes x0 -> zin
-            GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
-            return Lc::template col<C_G_INIT_W>(b, st);
+            b.Tx0 = nullptr;
+            GD_TRY(Lc::template rf<RF_YA>(b, st));
+            GD_TRY(Lc::template col<C_G_INIT>(b, st));
+            b.o0 = a.o2;   // RIF_CLAMP writes x0 -> zin
+            b.Tw = a.Tx0;  // ... and its row spectra to slot 1 of the full-batch workspace
+            b.t_slot = 1;
+            return Lc::template rif<RIF_CLAMP>(b, st);
         });
     }
-    static int admm_iter_gauss(Args a0, hipStream_t st) {
+    static int admm_iter_gauss(Args a0, hipStream_t st0) {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
-        return for_chunks(a0, L, HALF + 2 * IMG, [&](const Args& a) {
+        a0.Tw = nullptr;
+        a0.Tx0 = a0.first ? a0.T : nullptr;  // x0 spectra left by admm_init_gauss (full-batch layout)
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_ONE>(a, st));
-            GD_TRY(Lc::template col<C_G_ITER>(a, st));
+            GD_TRY(a.first ? Lc::template col<C_G_ITER0>(a, st) : Lc::template col<C_G_ITER>(a, st));
             return Lc::template ri<RI_OUT1>(a, st);
         });
     }
-    static int admm_iter(Args a0, hipStream_t st) {
-        // a.a0 = z, a.a1 = u1 (RF reads), a.a2 = w; RI: a.o0 = u1, a.o1 = w, a.o2 = zin / out
-        return for_chunks(a0, L, 2 * HALF + 3 * IMG, [&](const Args& a) {
+    static int admm_iter(Args a0, hipStream_t st0) {
+        // Poisson: a.a0 = z, a.a1 = u1 (RF reads), a.a2 = w; RI: a.o0 = u1, a.o1 = w, a.o2 = zin / out
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_ITER>(a, st));
             GD_TRY(Lc::template col<C_ITER>(a, st));
             return Lc::template ri<RI_ITER>(a, st);
         });
     }
-    static int wiener(Args a0, hipStream_t st) {
-        return for_chunks(a0, L, 2 * HALF + IMG, [&](const Args& a) {
+    static int wiener(Args a0, hipStream_t st0) {
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_PSF_RAW>(a, st));
             GD_TRY(Lc::template col<C_WIENER>(a, st));
             return Lc::template ri<RI_OUT1>(a, st);
         });
     }
-    static int richardson_lucy(Args a0, int n_iters, hipStream_t st) {
+    static int richardson_lucy(Args a0, int n_iters, hipStream_t st0) {
         // a.o0 = x (output, also the iterate); otf kept in a.otf.  The whole iteration loop runs per
-        // chunk, so x, y, the OTF and the workspace stay cache-resident across all n_iters.
-        return for_chunks(a0, L, 2 * HALF + 2 * IMG, [&](const Args& a) {
+        // chunk, so x, y, the OTF and the chunk's spectra stay cache-resident across all n_iters.
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_PSF_YP>(a, st));
             if (n_iters <= 0) return GD_OK;
             GD_TRY(Lc::template col<C_OTF_CONV>(a, st));
@@ -877,6 +1005,10 @@ extern "C" {
 
 int gd_abi_version(void) { return GD_ABI_VERSION; }
 
+// bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
+// profile is never reported against a different engine
+const char* gd_engine_rev(void) { return "r01.7-pipelined"; }
+
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
 int gd_supported_size(int H, int W) {
@@ -938,20 +1070,23 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
 size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
     if (!gd_supported_size(H, W) || N <= 0) return 0;
     const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
-    return llh == GD_LLH_GAUSSIAN ? 4 * spec : spec + 2 * img;
+    return llh == GD_LLH_GAUSSIAN ? spec / 2 + 3 * spec : spec + 2 * img;
 }
 
 namespace {
-// state layout - Gaussian: [otf | F(y/alpha) | F(u1) | F(v-u2)] (spectral); Poisson: [otf | u1 | w]
+// state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral);
+// Poisson: [otf | u1 | w]
 void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H;
     float2* base = reinterpret_cast<float2*>(state);
-    a.otf = base;
     if (llh == GD_LLH_GAUSSIAN) {
-        a.s_yal = base + spec;
-        a.s_u1 = base + 2 * spec;
-        a.s_w = base + 3 * spec;
+        a.s_hh = reinterpret_cast<float*>(base);
+        float2* c = base + spec / 2;  // spec is even (H even)
+        a.s_g = c;
+        a.s_u1 = c + spec;
+        a.s_w = c + 2 * spec;
     } else {
+        a.otf = base;
         float* u1 = reinterpret_cast<float*>(base + spec);
         a.o0 = u1;                       // u1 (spatial)
         a.o1 = u1 + (size_t)N * H * W;   // w = v - u2 (spatial)
@@ -973,6 +1108,7 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     a.llh = llh;
     bind_state(a, state, N, H, W, llh);
     a.o2 = zin;
+    ProfScope ps("op_admm_init<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN)
         return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
@@ -996,6 +1132,7 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     a.llh = llh;
     a.last = last;
     a.first = iter == 0;
+    ProfScope ps("op_admm_iter<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN) {
         a.a0 = z;
         a.o0 = zin_or_out;
@@ -1032,9 +1169,9 @@ int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, 
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
 }
 
-int gd_profile_enable(int on) {
+int gd_profile_enable(int level) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    g_prof_on = on != 0;
+    g_prof_level = level < 0 ? 0 : level;
     return GD_OK;
 }
 
@@ -1080,12 +1217,18 @@ size_t gd_set_chunk_bytes(size_t bytes) {
     return old;
 }
 
+int gd_set_pipeline_streams(int streams) {
+    const int old = g_pipe_streams;
+    if (streams >= 1) g_pipe_streams = streams < kMaxPipe ? streams : kMaxPipe;
+    return old;
+}
+
 int gd_subnet_param_count(void) { return gd::subnet::kParams; }
 
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
     if (N == 0) return GD_OK;
-    ProfScope ps("k_subnet_features<128,0>", (hipStream_t)stream);
+    ProfScope ps("k_subnet_features<128,0>", (hipStream_t)stream, 1);
     hipLaunchKernelGGL(gd::subnet::k_subnet_features, dim3(N), dim3(gd::subnet::kThreads), 0, (hipStream_t)stream,
                        reinterpret_cast<const float2*>(otf128_half), params, feat, N);
     return check_launch("k_subnet_features");

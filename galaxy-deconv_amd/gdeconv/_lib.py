@@ -23,6 +23,7 @@ _SZ = ctypes.c_size_t
 # name -> (restype, argtypes); must match include/gdeconv.h exactly (checked by tests/test_abi.py)
 SIGNATURES = {
     "gd_abi_version": (_I, []),
+    "gd_engine_rev": (ctypes.c_char_p, []),
     "gd_last_error": (ctypes.c_char_p, []),
     "gd_supported_size": (_I, [_I, _I]),
     "gd_workspace_bytes": (_SZ, [_I, _I, _I]),
@@ -38,6 +39,7 @@ SIGNATURES = {
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
     "gd_set_chunk_bytes": (_SZ, [_SZ]),
+    "gd_set_pipeline_streams": (_I, [_I]),
     "gd_subnet_param_count": (_I, []),
     "gd_subnet_features": (_I, [_P, _P, _P, _I, _P]),
     "gd_profile_enable": (_I, [_I]),
@@ -72,8 +74,9 @@ def load(path=LIB_PATH):
     return lib
 
 
-def profile_enable(on=True):
-    load().gd_profile_enable(int(bool(on)))
+def profile_enable(level=2):
+    """0 off, 1 whole operations only, 2 operations + every kernel launch."""
+    load().gd_profile_enable(int(level))
 
 
 def profile_reset():

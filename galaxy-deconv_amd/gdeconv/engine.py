@@ -193,14 +193,21 @@ class ADMMState:
         self.llh = _lib.GD_LLH[llh]
         dev = self.y.device
         nbytes = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W, self.llh))
-        self.ws = workspace(self.N, self.H, self.W, dev)   # validates the size first
+        workspace(self.N, self.H, self.W, dev)   # validates the size
+        # a private workspace: the Gaussian path keeps x0's spectra in it from init to iteration 0,
+        # so a denoiser that itself calls the engine cannot clobber it
+        self.ws = torch.empty(max(16, int(self.lib.gd_workspace_bytes(max(self.N, 1), self.H, self.W))),
+                              dtype=torch.uint8, device=dev)
         self.state = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         self.zin = torch.empty_like(self.y)
         self.iter = 0
 
     @property
     def otf(self):
-        """Half-spectrum OTF [N, W//2+1, H] (a view of the state buffer)."""
+        """Half-spectrum OTF [N, W//2+1, H] (Poisson state only; the Gaussian state keeps |H|^2 and
+        conj(H) F(y/alpha) instead)."""
+        if self.llh != _lib.GD_LLH["Poisson"]:
+            raise AttributeError("the Gaussian ADMM state stores |H|^2, not the OTF")
         K = self.W // 2 + 1
         return self.state[: self.N * K * self.H * 8].view(torch.complex64).view(self.N, K, self.H)
 

@@ -43,6 +43,7 @@ extern "C" {
 #define GD_LLH_POISSON 1
 
 int gd_abi_version(void);
+const char* gd_engine_rev(void);
 const char* gd_last_error(void);
 int gd_supported_size(int H, int W);
 size_t gd_workspace_bytes(int N, int H, int W);
@@ -64,9 +65,11 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
 
 /* Unrolled ADMM.  The per-forward state lives in an opaque device buffer of
  * gd_admm_state_bytes(N,H,W,llh) bytes whose first gd_otf_bytes(N,H,W) bytes are the half-spectrum
- * OTF.  llh = GD_LLH_GAUSSIAN keeps u1, v - u2 and F(max(y,0)/alpha) in the SPECTRAL domain (every
- * step of the Gaussian iteration is linear, so one forward and one inverse transform per iteration
- * suffice); GD_LLH_POISSON (sqrt in the V step) keeps u1 and v - u2 as images.
+ * OTF (Poisson).  llh = GD_LLH_GAUSSIAN keeps the state in the SPECTRAL domain - |H|^2,
+ * conj(H) F(max(y,0)/alpha), F(u1), conj(H) F(v - u2) - since every step of the Gaussian iteration is
+ * linear: one forward and one inverse transform per iteration.  GD_LLH_POISSON (sqrt in the V step)
+ * keeps the OTF and u1, v - u2 as images.  The Gaussian path also hands x0's spectra from
+ * gd_admm_init to the first gd_admm_iter through `ws`: keep the same workspace, untouched, in between.
  *
  * gd_admm_init: OTF, x0 = clamp(init_l2) -> zin (the first denoiser input, x0 + u1 with u1 = 0),
  *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].
@@ -100,16 +103,21 @@ int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, 
 int gd_subnet_param_count(void);
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream);
 
-/* Infinity-Cache chunking: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
- * run over the batch in chunks whose working set is about `bytes` (default 96 MiB), so spectra stay
- * resident in the 256 MiB Infinity Cache between kernels.  0 = whole batch per kernel.  Returns the
- * previous value.  Process-wide; set it before enqueuing work. */
+/* Infinity-Cache pipelining: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
+ * run over the batch in chunks of about `bytes` of workspace (default 96 MiB, i.e. 186 galaxies at
+ * 256^2); consecutive chunks go to internal HIP streams (default 2) forked from and joined back into
+ * the caller's stream, so each chunk's spectra stay resident in the 256 MiB Infinity Cache while the
+ * chip stays full.  bytes = 0: one pass over the batch.  Both setters return the previous value;
+ * process-wide, set them before enqueuing work. */
 size_t gd_set_chunk_bytes(size_t bytes);
+int gd_set_pipeline_streams(int streams);
 
-/* Opt-in per-kernel timing: when enabled, every kernel launch is bracketed by hipEvents on its
- * stream.  gd_profile_collect() waits for them and returns the number of distinct kernels;
+/* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,
+ * the SubNet kernel) on the caller's stream; level 2 also brackets every kernel launch on its own
+ * stream (adds two event records per launch - under pipelining that perturbs what it measures).
+ * gd_profile_collect() waits for the events and returns the number of distinct entries;
  * gd_profile_get(i, ...) reads the i-th (name, total ms, launches); gd_profile_reset() clears. */
-int gd_profile_enable(int on);
+int gd_profile_enable(int level);
 int gd_profile_collect(void);
 int gd_profile_get(int i, char* name, int name_len, double* total_ms, long long* launches);
 int gd_profile_reset(void);

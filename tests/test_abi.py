@@ -64,6 +64,6 @@ def test_argument_errors_need_no_device(lib):
     assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 50, 50, None, None) == -2
     assert lib.gd_admm_init(None, None, 0, 48, 48, None, 0, None, 0, 7, 1, 48, 48,
                             None, None, None, None) == -1
-    # state: Gaussian keeps OTF + F(y/alpha) + F(u1) + F(v-u2); Poisson OTF + two images
-    assert lib.gd_admm_state_bytes(3, 48, 48, 0) == 4 * 3 * 25 * 48 * 8
+    # state: Gaussian |H|^2 (fp32) + conj(H)F(y/a) + F(u1) + conj(H)F(v-u2); Poisson OTF + two images
+    assert lib.gd_admm_state_bytes(3, 48, 48, 0) == 3 * 25 * 48 * (4 + 3 * 8)
     assert lib.gd_admm_state_bytes(3, 48, 48, 1) == 3 * 25 * 48 * 8 + 2 * 3 * 48 * 48 * 4

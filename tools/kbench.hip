@@ -35,6 +35,27 @@ __global__ __launch_bounds__(256) void k_stream4(const float4* __restrict__ in, 
     }
 }
 
+// copy variants for the achievable-bandwidth ceiling
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copy_u(const f4v* __restrict__ in, f4v* __restrict__ out, size_t n4) {
+    const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    f4v v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n4) v[u] = NT ? __builtin_nontemporal_load(in + i) : in[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n4) {
+            if (NT) __builtin_nontemporal_store(v[u], out + i);
+            else out[i] = v[u];
+        }
+    }
+}
+
 template <typename F>
 float time_ms(F&& f, int reps = 10) {
     hipEvent_t a, b;
@@ -66,7 +87,7 @@ int main(int argc, char** argv) {
 
     Args a;
     memset(&a, 0, sizeof(a));
-    a.N = N; a.T = T; a.otf = state; a.s_yal = state + spec; a.s_u1 = state + 2 * spec; a.s_w = state + 3 * spec;
+    a.N = N; a.T = T; a.s_hh = (float*)state; a.s_g = state + spec / 2; a.s_u1 = a.s_g + spec; a.s_w = a.s_g + 2 * spec;
     a.y = y; a.a0 = z; a.o0 = zin;
     a.alpha = a.rho1 = a.rho2 = a.rho2n = GalScalar{par, 1};
     a.llh = GD_LLH_GAUSSIAN; a.first = 0; a.last = 0;
@@ -85,11 +106,18 @@ int main(int argc, char** argv) {
     printf("k_col<G_ITER>  prod %.3f ms (%.2f TB/s) | no-FFT %.3f ms (%.2f) | prefetch H,W %.3f ms (%.2f)\n",
            t0, colgb / t0, t1, colgb / t1, t2, colgb / t2);
 
-    const int rg1 = N * (L / RowGeo<L, 1>::RB);
-    float tf = time_ms([&] { hipLaunchKernelGGL((k_row_fwd<L, RF_ONE>), dim3(rg1), dim3(RowGeo<L, 1>::THREADS), 0, 0, a); });
-    float ti = time_ms([&] { hipLaunchKernelGGL((k_row_inv<L, RI_OUT1>), dim3(rg1), dim3(RowGeo<L, 1>::THREADS), 0, 0, a); });
-    printf("k_row_fwd<ONE> %.3f ms (%.2f TB/s) | k_row_inv<OUT1> %.3f ms (%.2f TB/s)\n",
-           tf, (img_gb + half_gb) / tf, ti, (img_gb + half_gb) / ti);
+    auto rows = [&](auto rbx) {
+        constexpr int RBX = decltype(rbx)::value;
+        using R = RowGeo<L, 1, RBX>;
+        const int grid = N * (L / R::RB);
+        float tf = time_ms([&] { hipLaunchKernelGGL((k_row_fwd<L, RF_ONE, RBX>), dim3(grid), dim3(R::THREADS), 0, 0, a); });
+        float ti = time_ms([&] { hipLaunchKernelGGL((k_row_inv<L, RI_OUT1, RBX>), dim3(grid), dim3(R::THREADS), 0, 0, a); });
+        printf("rows/block %3d (%4d thr, LDS %6d B): k_row_fwd<ONE> %.3f ms (%.2f TB/s) | k_row_inv<OUT1> %.3f ms (%.2f TB/s)\n",
+               R::RB, R::THREADS, R::LDS * 8, tf, (img_gb + half_gb) / tf, ti, (img_gb + half_gb) / ti);
+    };
+    rows(std::integral_constant<int, 16>{});
+    rows(std::integral_constant<int, 0>{});
+    rows(std::integral_constant<int, 64>{});
 
     // calibration: same bytes as k_col (5 reads + 3 writes of a half spectrum) as float4 streams
     const size_t n4 = spec * 8 / 16;
@@ -99,5 +127,57 @@ int main(int argc, char** argv) {
     float tc = time_ms([&] { hipLaunchKernelGGL((k_stream4<1, 1>), dim3(8192), dim3(256), 0, 0,
                                                 (const float4*)state, (float4*)T, n4 * 2); });
     printf("copy float4 (%.2f GB) %.3f ms (%.2f TB/s)\n", 4 * half_gb, tc, 4 * half_gb / tc);
+    // ---- full Gaussian iteration RF(z) -> C -> RI(zin): one pass over the batch vs chunks on S streams
+    {
+        const int rg1 = RowGeo<L, 1>::RB;
+        auto launch_iter = [&](const Args& b, float2* Tb, hipStream_t st) {
+            Args c = b;
+            c.T = Tb;
+            hipLaunchKernelGGL((k_row_fwd<L, RF_ONE>), dim3(c.N * (L / rg1)), dim3(RowGeo<L, 1>::THREADS), 0, st, c);
+            hipLaunchKernelGGL((k_col<L, C_G_ITER>), dim3((c.N * K + Gm::LPB - 1) / Gm::LPB), dim3(256), 0, st, c);
+            hipLaunchKernelGGL((k_row_inv<L, RI_OUT1>), dim3(c.N * (L / rg1)), dim3(RowGeo<L, 1>::THREADS), 0, st, c);
+        };
+        const double iter_gb = N * (2.0 * (L * L * 4) + 11.5 * (K * L * 8)) / 1e9;
+        float tfull = time_ms([&] { launch_iter(a, T, 0); });
+        printf("iteration, one pass   : %.3f ms (%.2f TB/s algorithmic)\n", tfull, iter_gb / tfull);
+        const int SMAX = 4;
+        hipStream_t str[SMAX];
+        for (int i = 0; i < SMAX; ++i) CK(hipStreamCreateWithFlags(&str[i], hipStreamNonBlocking));
+        hipEvent_t ev0, evs[SMAX];
+        CK(hipEventCreateWithFlags(&ev0, hipEventDisableTiming));
+        for (int i = 0; i < SMAX; ++i) CK(hipEventCreateWithFlags(&evs[i], hipEventDisableTiming));
+        for (int S : {2, 3, 4})
+            for (int G : {64, 96, 128, 160, 192}) {
+                if ((size_t)S * G > (size_t)N) continue;
+                float t = time_ms([&] {
+                    CK(hipEventRecord(ev0, 0));
+                    for (int i = 0; i < S; ++i) CK(hipStreamWaitEvent(str[i], ev0, 0));
+                    for (int g0 = 0, c = 0; g0 < N; g0 += G, ++c) {
+                        const int n = N - g0 < G ? N - g0 : G;
+                        Args b = offset_args(a, g0, n, L);
+                        launch_iter(b, T + (size_t)(c % S) * 2 * G * K * L, str[c % S]);
+                    }
+                    for (int i = 0; i < S; ++i) {
+                        CK(hipEventRecord(evs[i], str[i]));
+                        CK(hipStreamWaitEvent(0, evs[i], 0));
+                    }
+                });
+                printf("iteration, chunks of %4d on %d streams: %.3f ms (%.2f TB/s algorithmic)\n", G, S, t, iter_gb / t);
+            }
+    }
+
+    auto cu = [&](auto u, auto nt) {
+        constexpr int U = decltype(u)::value;
+        constexpr bool NT = decltype(nt)::value;
+        const size_t n = n4 * 2;
+        const int grid = (int)((n + 256 * U - 1) / (256 * U));
+        float t = time_ms([&] { hipLaunchKernelGGL((k_copy_u<U, NT>), dim3(grid), dim3(256), 0, 0,
+                                                   (const f4v*)state, (f4v*)T, n); });
+        printf("copy x%d %s (%.2f GB) %.3f ms (%.2f TB/s)\n", U, NT ? "nt" : "  ", 4 * half_gb, t, 4 * half_gb / t);
+    };
+    cu(std::integral_constant<int, 1>{}, std::false_type{});
+    cu(std::integral_constant<int, 4>{}, std::false_type{});
+    cu(std::integral_constant<int, 8>{}, std::false_type{});
+    cu(std::integral_constant<int, 4>{}, std::true_type{});
     return 0;
 }

@@ -16,9 +16,9 @@ import json
 import re
 
 MODE_NAMES = {
-    "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO"],
+    "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO", "YA"],
     "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV",
-              "G_OTF_INIT", "G_INIT_W", "G_ITER"],
+              "G_INIT", "G_ITER", "G_ITER0"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES"],
@@ -57,7 +57,11 @@ def main():
     a = ap.parse_args()
     fetch, nf = per_launch(a.fetch, "FETCH_SIZE")
     write, _ = per_launch(a.write, "WRITE_SIZE")
-    out = {"batch": a.batch, "size": a.size,
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "galaxy-deconv_amd"))
+    from gdeconv import _lib
+    out = {"batch": a.batch, "size": a.size, "engine_rev": _lib.load().gd_engine_rev().decode(),
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH_SIZE x2 (gfx950 "
                      "half-counting of wide streaming reads, MI355X_MICROARCH.md HBM section); KiB -> bytes",
            "kernels": {}}
