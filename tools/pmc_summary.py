@@ -54,6 +54,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=16,
+                    help="ADMM iterations in the profiled run (bench --steps 1 --warmup 1: 2 x 8)")
     a = ap.parse_args()
     fetch, nf = per_launch(a.fetch, "FETCH_SIZE")
     write, _ = per_launch(a.write, "WRITE_SIZE")
@@ -70,6 +72,15 @@ def main():
         wr = write.get(k, 0.0) * 1024
         out["kernels"][k] = {"read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                              "hbm_bytes_per_launch": rd + wr, "launches": nf.get(k, 0)}
+    # whole Gaussian ADMM iteration (RF(z) -> C_G_ITER[0] -> RI(zin), all chunks): traffic per call
+    L = a.size
+    members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER0>", f"k_row_inv<{L},OUT1>"]
+    tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in out["kernels"].items() if k in members)
+    if tot:
+        out["kernels"][f"op_admm_iter<{L},Gaussian>"] = {
+            "hbm_bytes_per_launch": tot / a.iters, "launches": a.iters,
+            "note": "sum over the iteration's RF/C/RI chunk launches; FETCH/WRITE_SIZE count L2<->fabric "
+                    "traffic, Infinity-Cache hits included"}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out["kernels"].items():
         print(f"{k:28s} read {v['read_bytes_per_launch'] / 1e9:8.3f} GB  write {v['write_bytes_per_launch'] / 1e9:8.3f} GB")
