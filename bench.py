@@ -220,14 +220,16 @@ def main():
     ops = {k: v for k, v in kstats.items() if k.startswith("op_")}
     kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
     pipelined = chunk_bytes > 0
-    if pipelined and ops and not kern:
+    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n)}
+    if pipelined and priced_ops:
         # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
         # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
-        dom_raw = max(ops, key=lambda k: ops[k][0])
+        dom_raw = max(priced_ops, key=lambda k: ops[k][0])
         dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
         per_gal = op_bytes(dom_raw, L, n)
     else:
-        dom_raw = max(kern, key=lambda k: kern[k][0])
+        priced = {k: v for k, v in kern.items() if kernel_bytes(k, L, n)} or kern
+        dom_raw = max(priced, key=lambda k: kern[k][0])
         dom_ms = kern[dom_raw][0] / kern[dom_raw][1]
         per_gal = kernel_bytes(dom_raw, L, n)
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None

@@ -26,7 +26,9 @@ MODE_NAMES = {
 
 
 def pretty(kname):
-    m = re.search(r"(k_\w+)<(\d+), (\d+)>", kname)
+    if "k_subnet_features" in kname:
+        return "k_subnet_features<128,FEATURES>"
+    m = re.search(r"(k_\w+)<(\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
         return None
     k, L, mode = m.group(1), m.group(2), int(m.group(3))
@@ -83,7 +85,11 @@ def main():
                     "traffic, Infinity-Cache hits included"}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out["kernels"].items():
-        print(f"{k:28s} read {v['read_bytes_per_launch'] / 1e9:8.3f} GB  write {v['write_bytes_per_launch'] / 1e9:8.3f} GB")
+        if "read_bytes_per_launch" in v:
+            print(f"{k:28s} read {v['read_bytes_per_launch'] / 1e9:8.3f} GB  write "
+                  f"{v['write_bytes_per_launch'] / 1e9:8.3f} GB  x{v['launches']}")
+        else:
+            print(f"{k:28s} total {v['hbm_bytes_per_launch'] / 1e9:8.3f} GB per call  x{v['launches']}")
 
 
 if __name__ == "__main__":
