@@ -31,10 +31,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s m
 MODE_NAMES = {
     "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO", "YA"],
     "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV",
-              "G_INIT", "G_ITER", "G_ITER0"],
+              "G_INIT", "G_ITER", "G_W1", "G_ITER_F", "G_ITER_L", "G_ITER_FL"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES"],
+    "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
 }
 
 
@@ -46,13 +47,20 @@ def pretty(name):
     return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
 
 
-def op_bytes(name, L, n_iters):
-    """Algorithmic bytes per galaxy of one whole engine operation (its kernels' compulsory traffic):
-    Gaussian ADMM iteration = RF(z) + C_G_ITER + RI(zin), averaged over first / middle / last."""
+def op_bytes(name, L, n_iters, fused=False):
+    """Algorithmic bytes per galaxy of one whole engine operation (its kernels' compulsory traffic),
+    averaged over the first / middle / last ADMM iteration.  Gaussian iteration, fused (k_gal_iter):
+    z + state (|H|^2, G, U1, W~) in, U1, W~ + zin out = 2 img + 5.5 half (first: no U1 read; last: no
+    G read, no state written); three-kernel: RF(z) + C_G_ITER + RI(zin) adds the workspace round trips."""
     img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
     if pretty(name) == f"op_admm_iter<{L},Gaussian>":
-        c = (6.5 + 7.5 * max(0, n - 2) + 4.5 * (n > 1)) / n
-        return 2 * img + (2 + c) * half
+        if n == 1:
+            c = 1.5 if fused else 5.5
+        elif fused:
+            c = (4.5 + 5.5 * (n - 2) + 2.5) / n
+        else:
+            c = (2 + 6.5 + (2 + 7.5) * (n - 2) + 2 + 4.5) / n
+        return 2 * img + c * half
     return None
 
 
@@ -67,8 +75,13 @@ def kernel_bytes(name, L, n_iters):
     table = {
         # Gaussian (spectral state |H|^2, G = conj(H)F(y/a), U1, W~ = conj(H)W): RF(z) -> C_G_ITER -> RI(zin)
         f"k_row_fwd<{L},ONE>": img + half,                                  # z -> T
-        f"k_col<{L},G_ITER>": half * (7.5 * max(0, n - 2) + 4.5 * (n > 1)) / max(1, n - 1),  # T,|H|^2,G,U1,W~ -> U1,W~,T
-        f"k_col<{L},G_ITER0>": half * 6.5,                                  # T, x0 T, |H|^2, G -> U1, W~, T
+        f"k_col<{L},G_ITER>": half * 7.5,                                   # T, |H|^2, G, U1, W~ -> U1, W~, T
+        f"k_col<{L},G_ITER_F>": half * 6.5,                                 # T, |H|^2, G, W~ -> U1, W~, T
+        f"k_col<{L},G_ITER_L>": half * 4.5,                                 # T, |H|^2, U1, W~ -> T
+        f"k_col<{L},G_W1>": half * 3.5,                                     # x0 T, |H|^2, G -> W~
+        f"k_gal_iter<{L},MID>": 2 * img + 5.5 * half,                       # z, |H|^2, G, U1, W~ -> U1, W~, zin
+        f"k_gal_iter<{L},FIRST>": 2 * img + 4.5 * half,
+        f"k_gal_iter<{L},LAST>": 2 * img + 2.5 * half,
         f"k_row_inv<{L},OUT1>": half + img,                                 # T -> zin | x
         f"k_row_fwd<{L},YA>": img + half,                                   # y -> T
         f"k_col<{L},G_INIT>": half + 2.5 * half,                            # T -> |H|^2, G, T (PSF: 9 KB)
@@ -108,6 +121,7 @@ def parse():
     p.add_argument("--chunk-mb", type=float, default=None,
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
+    p.add_argument("--fused", type=int, default=None, help="1: one-kernel Gaussian iteration (256^2), 0: three kernels")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
     return p.parse_args()
@@ -164,6 +178,11 @@ def main():
         lib.gd_set_chunk_bytes(int(args.chunk_mb * (1 << 20)))
     chunk_bytes = lib.gd_set_chunk_bytes(0)
     lib.gd_set_chunk_bytes(chunk_bytes)
+    if args.fused is not None:
+        lib.gd_set_fused_iteration(args.fused)
+    fused = lib.gd_set_fused_iteration(0)
+    lib.gd_set_fused_iteration(fused)
+    use_fused = bool(fused) and args.size == 256 and args.llh == "Gaussian"
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
     pipe_streams = lib.gd_set_pipeline_streams(0)
@@ -220,13 +239,13 @@ def main():
     ops = {k: v for k, v in kstats.items() if k.startswith("op_")}
     kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
     pipelined = chunk_bytes > 0
-    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n)}
-    if pipelined and priced_ops:
+    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused)}
+    if (pipelined or use_fused) and priced_ops:
         # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
         # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
         dom_raw = max(priced_ops, key=lambda k: ops[k][0])
         dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
-        per_gal = op_bytes(dom_raw, L, n)
+        per_gal = op_bytes(dom_raw, L, n, use_fused)
     else:
         priced = {k: v for k, v in kern.items() if kernel_bytes(k, L, n)} or kern
         dom_raw = max(priced, key=lambda k: kern[k][0])
@@ -260,7 +279,8 @@ def main():
                                f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])",
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
                    "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
-                   "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1},
+                   "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
+                   "iteration": "fused (k_gal_iter, one workgroup per galaxy)" if use_fused else "three-kernel"},
         "roofline": roofline,
         "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},

@@ -75,12 +75,11 @@ struct Args {
     float2* s_w;           //   conj(H) F(v - u2)
     int t_slot;            // image slot of T that row-forward kernels write (RIF_CLAMP -> 1)
     float2* Tw;            // if set: row-forward kernels write here (full-batch layout) instead of T
-    float2* Tx0;           // Gaussian iteration 0: x0's row spectra (slot 1, full-batch layout)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA };
 enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV,
-               C_G_INIT, C_G_ITER, C_G_ITER0 };
+               C_G_INIT, C_G_ITER, C_G_W1, C_G_ITER_F, C_G_ITER_L, C_G_ITER_FL };  // _F first, _L last iteration
 enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
 enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
@@ -277,14 +276,46 @@ struct ColTraits {
     static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
                                  MODE == C_WIENER || MODE == C_CONV2);
     static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
-    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD);
+    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_W1);
     static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
     static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2);
     static constexpr bool FWD = (MODE != C_INV);
 };
 
-// VAR: experiment switch for tools/kbench.hip (0 = production; 1 = no FFTs, memory only;
-// 2 = G_ITER operands H and W loaded before the forward FFT)
+// Gaussian ADMM iteration for one spectral element, entirely in the spectral domain (every step of
+// models/Unrolled_ADMM.py:207-213 is linear for llh='Gaussian'), with the v - u2 state kept
+// premultiplied by conj(H) (W~ = conj(H) W) so only |H|^2 and G are needed:
+//   X    = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2 + rho2)        X_Update :315-319
+//   U1'  = (U1 + X) - Z                                            :212
+//   U2~  = |H|^2 X - W~                     (= conj(H) (H X - W))   :213
+//   V~   = (rho2' (|H|^2 X + U2~) + G) / (1 + rho2')               V step :335-336
+//   W~'  = V~ - U2~ ;  returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last iteration)
+// First iteration: U1 = 0 (not read); W~ = conj(H) V1 was written by the init (C_G_W1).
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ float2 gauss_iter_elem(const Args& a, size_t o, float2 Zk, float r1, float r2,
+                                                  float r2n, bool valid, float inv_n) {
+    const float hh = a.s_hh[o];
+    float2 U1 = make_float2(0.f, 0.f), Gk = make_float2(0.f, 0.f);
+    if constexpr (!LAST) Gk = a.s_g[o];
+    if constexpr (!FIRST) U1 = a.s_u1[o];
+    const float2 Wt = a.s_w[o];
+    const float lhs = r1 * hh + r2;
+    const float2 A = csub(Zk, U1);
+    const float2 X = make_float2((r1 * A.x + r2 * Wt.x) / lhs, (r1 * A.y + r2 * Wt.y) / lhs);
+    if constexpr (LAST) return cscale(X, inv_n);
+    const float2 U1n = csub(cadd(U1, X), Zk);
+    const float2 HHX = cscale(X, hh);
+    const float2 U2t = csub(HHX, Wt);
+    const float d = 1.0f + r2n;
+    const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
+    if (valid) {
+        a.s_u1[o] = U1n;
+        a.s_w[o] = csub(Vt, U2t);
+    }
+    return cscale(cadd(X, U1n), inv_n);
+}
+
+// VAR: experiment switch for tools/kbench.hip (0 = production; 1 = no FFTs, memory only)
 template <int L, int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) void k_col(Args a) {
     using G = Geo<L>;
@@ -305,41 +336,30 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     const size_t c0 = tidx(g, 0, kx, 0, K, L), c1 = tidx(g, 1, kx, 0, K, L);
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
-        P[s] = a.T[c0 + j + F1 * s];
+        P[s] = a.T[(MODE == C_G_W1 ? c1 : c0) + j + F1 * s];  // C_G_W1: x0's row spectra in slot 1
         if constexpr (TR::IN2) Q[s] = a.T[c1 + j + F1 * s];
-    }
-    constexpr bool gfirst = (MODE == C_G_ITER0);  // iteration 0: x0's row spectra wait in Tx0 slot 1
-    if constexpr (gfirst) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) Q[s] = a.Tx0[c1 + j + F1 * s];
-    }
-    float2 Hpre[VAR == 2 ? F2 : 1], Wpre[VAR == 2 ? F2 : 1];
-    if constexpr (VAR == 2 && MODE == C_G_ITER) {
-        const size_t ob0 = ((size_t)g * K + kx) * L;
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            Hpre[s] = make_float2(0.f, 0.f);
-            Wpre[s] = a.s_w[ob0 + j + F1 * s];
-        }
     }
     __syncthreads();  // twiddles
     if constexpr (TR::FWD && VAR != 1) {
         line_fft<L, false>(P, j, my, tw);
         if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
-        if constexpr (gfirst) line_fft<L, false>(Q, j, my, tw);
     }
     // C_G_INIT: the OTF column H(., kx) straight from the h x h PSF: row DFT at kx of the (at most h)
-    // non-zero rows of the circularly shifted, zero-padded PSF, then the column FFT.  The PSFs of the
-    // (at most two) galaxies this block touches are staged in LDS (rows padded to h+1).
+    // non-zero rows of the circularly shifted, zero-padded PSF, then the column FFT.  The block first
+    // computes the row-DFT values S[i][line] for its LPB columns cooperatively (lanes of a 16-group
+    // share the PSF row i -> broadcast reads; no divergence), in the exchange area, optionally after
+    // the PSFs of the (at most NGB) galaxies it touches staged in LDS with rows padded to h+1.
     float2 Hc[MODE == C_G_INIT ? F2 : 1];
     if constexpr (MODE == C_G_INIT) {
         const int h = a.h, hp = h + 1, c0p = h >> 1;
         constexpr int NGB = (G::LPB + K - 2) / K + 1;                  // galaxies a block can touch
         const int gb = (blockIdx.x * G::LPB) / K;                      // first galaxy of the block
-        const bool staged = NGB * h * hp <= G::COL_LDS * 2;
+        const int pst = (NGB * h * hp + 1) & ~1;                        // staged floats (even)
+        const bool staged = pst + 2 * G::LPB * h <= G::COL_LDS * 2;
         float* pl = reinterpret_cast<float*>(xch);
+        float2* S = staged ? reinterpret_cast<float2*>(pl + pst) : xch;  // [h][LPB]
+        __syncthreads();  // (the forward FFT above used xch)
         if (staged) {
-            __syncthreads();  // (the forward FFT above used xch)
             const int ng = (a.N - gb < NGB) ? a.N - gb : NGB;
             for (int q = tid; q < ng * h * h; q += 256) {
                 const int gg = q / (h * h), rem = q - gg * h * h, i = rem / h, jj = rem - i * h;
@@ -347,46 +367,55 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             }
             __syncthreads();
         }
-        const float* ps = staged ? pl + (g - gb) * h * hp : a.psf + (long long)g * a.psf_gstride;
-        const int ld = staged ? hp : h;
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            int i = j + F1 * s + c0p;
-            if (i >= L) i -= L;
+        const int cst = (L - c0p) % L;  // padded column of psf column 0
+        for (int o = tid; o < G::LPB * h; o += 256) {
+            const int i = o / G::LPB, ln = o - i * G::LPB;
+            const int fo = blockIdx.x * G::LPB + ln;
             float2 acc0 = make_float2(0.f, 0.f), acc1 = acc0;
-            if (i < h) {
-                const float* row = ps + i * ld;
-                int c = (L - c0p) % L;                 // column offset of jj = 0
+            if (fo < a.N * K) {
+                const int go = fo / K, kxo = fo - go * K;
+                const float* row = staged ? pl + ((go - gb) * h + i) * hp
+                                          : a.psf + (long long)go * a.psf_gstride + (long long)i * h;
+                int idx = (kxo * cst) % L;   // twiddle index kx * c (mod L), c = column of jj
                 int jj = 0;
-                for (; jj + 1 < h; jj += 2) {           // two independent accumulators
-                    const int c1 = (c + 1 == L) ? 0 : c + 1;
-                    const float2 w0 = tw[(kx * c) % L], w1 = tw[(kx * c1) % L];
+                for (; jj + 1 < h; jj += 2) {  // two independent accumulators
+                    const float2 w0 = tw[idx];
+                    idx += kxo; if (idx >= L) idx -= L;
+                    const float2 w1 = tw[idx];
+                    idx += kxo; if (idx >= L) idx -= L;
                     const float v0 = row[jj], v1 = row[jj + 1];
                     acc0.x = fmaf(v0, w0.x, acc0.x);
                     acc0.y = fmaf(v0, w0.y, acc0.y);
                     acc1.x = fmaf(v1, w1.x, acc1.x);
                     acc1.y = fmaf(v1, w1.y, acc1.y);
-                    c = (c1 + 1 == L) ? 0 : c1 + 1;
                 }
                 if (jj < h) {
-                    const float2 w0 = tw[(kx * c) % L];
+                    const float2 w0 = tw[idx];
                     acc0.x = fmaf(row[jj], w0.x, acc0.x);
                     acc0.y = fmaf(row[jj], w0.y, acc0.y);
                 }
             }
-            Hc[s] = cadd(acc0, acc1);
+            S[i * G::LPB + ln] = cadd(acc0, acc1);
         }
-        if (staged) __syncthreads();  // PSF staging area -> exchange areas
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            int i = j + F1 * s + c0p;
+            if (i >= L) i -= L;
+            Hc[s] = (i < h) ? S[i * G::LPB + line] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();  // S -> exchange areas
         line_fft<L, false>(Hc, j, my, tw);
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
     const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_INIT) ? a.alpha(g) : 1.f;
-    constexpr bool giter = (MODE == C_G_ITER || MODE == C_G_ITER0);
+    constexpr bool giter = (MODE == C_G_ITER || MODE == C_G_ITER_F || MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
+    constexpr bool gfirst = (MODE == C_G_ITER_F || MODE == C_G_ITER_FL);
+    constexpr bool glast = (MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
     const float r1 = (MODE == C_ITER || giter) ? a.rho1(g) : 0.f;
     const float r2 = (MODE == C_ITER || giter) ? a.rho2(g) : 0.f;
-    const bool glast = giter && a.last;
-    const float r2n = (giter && !glast) ? a.rho2n(g) : 0.f;
+    const float r2n = ((giter && !glast) || MODE == C_G_W1) ? a.rho2n(g) : 0.f;
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
@@ -425,44 +454,15 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float lhs = hh + 1.0f / al;
             P[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
         } else if constexpr (giter) {
-            // Gaussian ADMM iteration entirely in the spectral domain (every step of
-            // models/Unrolled_ADMM.py:207-213 is linear for llh='Gaussian'), with the v - u2 state
-            // kept premultiplied by conj(H) (W~ = conj(H) W) so only |H|^2 and G are needed:
-            //   X    = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2 + rho2)        X_Update :315-319
-            //   U1'  = (U1 + X) - Z                                            :212
-            //   U2~  = |H|^2 X - W~                     (= conj(H) (H X - W))   :213
-            //   V~   = (rho2' (|H|^2 X + U2~) + G) / (1 + rho2')               V step :335-336
-            //   W~'  = V~ - U2~ ;  out = X + U1' (next denoiser input) | X (last iteration)
-            // First iteration: U1 = 0 and W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2).
-            const float2 Zk = P[s];
+            P[s] = gauss_iter_elem<gfirst, glast>(a, ob + ky, P[s], r1, r2, r2n, valid, inv_n);
+        } else if constexpr (MODE == C_G_W1) {
+            // iteration 0's W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2): the V step
+            // (models/Unrolled_ADMM.py:335-336) with Hx = H X0 and u2 = 0, premultiplied by conj(H)
             const float hh = a.s_hh[ob + ky];
-            float2 U1 = make_float2(0.f, 0.f), Wt, Gk = make_float2(0.f, 0.f);
-            if (gfirst || !glast) Gk = a.s_g[ob + ky];
-            if constexpr (gfirst) {
-                const float d0 = 1.0f + r2;
-                Wt = make_float2((r2 * (hh * Q[s].x + 0.0f) + Gk.x) / d0, (r2 * (hh * Q[s].y + 0.0f) + Gk.y) / d0);
-            } else {
-                U1 = a.s_u1[ob + ky];
-                if constexpr (VAR == 2) Wt = Wpre[s];
-                else Wt = a.s_w[ob + ky];
-            }
-            const float lhs = r1 * hh + r2;
-            const float2 A = csub(Zk, U1);
-            const float2 X = make_float2((r1 * A.x + r2 * Wt.x) / lhs, (r1 * A.y + r2 * Wt.y) / lhs);
-            if (glast) {
-                P[s] = cscale(X, inv_n);
-            } else {
-                const float2 U1n = csub(cadd(U1, X), Zk);
-                const float2 HHX = cscale(X, hh);
-                const float2 U2t = csub(HHX, Wt);
-                const float d = 1.0f + r2n;
-                const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
-                if (valid) {
-                    a.s_u1[ob + ky] = U1n;
-                    a.s_w[ob + ky] = csub(Vt, U2t);
-                }
-                P[s] = cscale(cadd(X, U1n), inv_n);
-            }
+            const float2 Gk = a.s_g[ob + ky];
+            const float d0 = 1.0f + r2n;
+            const float2 Wt = make_float2((r2n * (hh * P[s].x + 0.0f) + Gk.x) / d0, (r2n * (hh * P[s].y + 0.0f) + Gk.y) / d0);
+            if (valid) a.s_w[ob + ky] = Wt;
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
@@ -496,6 +496,242 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
                 a.T[c0 + j + F1 * s] = P[s];
                 if constexpr (TR::OUT2) a.T[c1 + j + F1 * s] = Q[s];
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fused whole-galaxy Gaussian iteration
+// One 1024-thread workgroup per galaxy, one workgroup per CU: the galaxy's half spectrum (264 KiB at
+// 256^2) lives in that CU's registers and LDS for the whole iteration, so the row spectra never go
+// to HBM.  z -> zin moves z, zin and the state (|H|^2, G, U1, W~ read; U1, W~ written): 7.5 fp32
+// words per pixel instead of the three-kernel path's 11.6.  Phases (S = LDS union):
+//   R  64 lines x L/(2*64) row pairs (rows 2p + i 2p+1): row FFT in registers
+//   A  the bins that columns 0..L/4-1 need (X_p[kx], X_p[L-kx]) -> S; column kx = line: gather the
+//      two rows' half spectra (split of the packed pair), column FFT, spectral update, column IFFT;
+//      line 0 also does the Nyquist column kx = L/2 (its bins wait in `nyq`); results stay in registers
+//   B  the same for columns L/4..L/2-1, whose bins waited in registers
+//   I  per half of the rows: column results -> S as row half spectra, row IFFT of the packed pairs,
+//      store (x for the last iteration, else zin = x + u1)
+#ifndef GD_FUSED_PARK
+#define GD_FUSED_PARK 3  // bit 0: park slice B's bins, bit 1: park slice A's results (see k_gal_iter)
+#endif
+#ifndef GD_FUSED_FFTBAR
+#define GD_FUSED_FFTBAR 1
+#endif
+#ifndef GD_FUSED_GROUP
+#define GD_FUSED_GROUP 4
+#endif
+// A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
+// (and kept live from) an earlier phase's identical computation.
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+template <int L>
+struct FusedGeo {
+    static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1;
+    static constexpr int THREADS = 1024, LINES = THREADS / F1;
+    static constexpr int NP = L / 2, PPL = NP / LINES;  // row pairs; pairs per line
+    static constexpr int KS = L / 4;                    // columns per slice (one per line)
+    static constexpr int SLD = 2 * KS + 4;              // S row stride (float2), >= K, 8 dwords mod 64 banks
+    static constexpr int XCH = xch_elems<L>();
+    static constexpr int U = cmax(NP * SLD, LINES * XCH);
+    static_assert(LINES == KS, "one column per line and slice");
+    static_assert(NP == 2 * LINES && PPL == 2, "two row pairs per line; half the rows per inverse pass");
+    static_assert(KS % F1 == 0 && (L / 2) % F1 == 0, "slice edges on lane-register boundaries");
+    static_assert(SLD >= K, "row half spectrum must fit a stride");
+};
+
+// Column c of a slice from S = [pair][SLD] holding X_p[kx] at [c] and X_p[(L - kx) mod L] at [KS + c]:
+// row y's half spectrum R_y[kx] = (X + conj X')/2 (y even) or (X - conj X')/(2i) (y odd).
+template <int L>
+__device__ __forceinline__ void fused_gather(const float2* S, int c, int j, float2 (&C)[FusedGeo<L>::F2]) {
+    using FG = FusedGeo<L>;
+    c = opaque(c);
+    j = opaque(j);
+#pragma unroll
+    for (int s = 0; s < FG::F2; ++s) {
+        const int y = j + FG::F1 * s;
+        const float2 u = S[(y >> 1) * FG::SLD + c], v = S[(y >> 1) * FG::SLD + FG::KS + c];
+        C[s] = (y & 1) ? make_float2(0.5f * (u.y + v.y), 0.5f * (v.x - u.x))
+                       : make_float2(0.5f * (u.x + v.x), 0.5f * (u.y - v.y));
+    }
+}
+
+template <int L, bool FIRST, bool LAST>
+__device__ __forceinline__ void fused_column(const Args& a, float2 (&C)[FusedGeo<L>::F2], int g, int kx, int j,
+                                             float2* my, const float2* tw, float r1, float r2, float r2n) {
+    using FG = FusedGeo<L>;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    j = opaque(j);
+    kx = opaque(kx);
+    line_fft<L, false, true>(C, j, my, tw);
+#if GD_FUSED_FFTBAR
+    __builtin_amdgcn_sched_barrier(0);  // keep the state loads below the FFT (register pressure)
+#endif
+    const size_t ob = ((size_t)g * FG::K + kx) * L;
+#pragma unroll
+    for (int s = 0; s < FG::F2; ++s) {
+        C[s] = gauss_iter_elem<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
+        if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
+    }
+    line_fft<L, true, true>(C, j, my, tw);
+}
+
+template <int L, bool FIRST, bool LAST>
+__global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
+    using FG = FusedGeo<L>;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
+    __shared__ float2 nyq[FG::NP];
+    __shared__ float2 xnyq[64 / F1 * FG::XCH];  // wave 0's exchange areas for the Nyquist column
+    __shared__ float nyqo[L];         // ... and its result (real parts)
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    float2* my = S + line * FG::XCH;
+    fill_twiddles<L>(tw, tid, FG::THREADS);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+
+    // R: pair p = line + LINES q
+    float2 X[FG::PPL][F2];
+    const float* z = a.a0 + (size_t)g * L * L;
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+    }
+    __syncthreads();  // twiddles
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
+    // Register budget (128 VGPRs at 1024 threads): what a later phase needs but the current one does
+    // not is parked in this galaxy's output image, written whole at the end (z is already in registers,
+    // so zin == z is fine): region 0 = slice B's bins (registers r in [RB0, RB1), the few at RB1 stay),
+    // region 1 = slice A's column results.  Lane-contiguous (512 B per wave instruction), read back
+    // by the same thread; region 0 is consumed before phase I writes rows 0..L/2-1 over it, and each
+    // half of region 1 before phase I writes rows L/2..L-1.
+    float2* park0 = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L);
+    float2* park1 = park0 + (size_t)L * L / 4;
+    constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
+    static_assert(FG::PPL * (RB1 - RB0) * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4, "park regions");
+    if constexpr (GD_FUSED_PARK & 1) {
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q)
+#pragma unroll
+            for (int r = RB0; r < RB1; ++r) park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + tid] = X[q][r];
+    }
+    __syncthreads();  // exchange areas -> slice A
+
+    // A: columns 0..KS-1 (+ Nyquist)
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        const int p = line + LINES * q;
+        float2* row = S + p * SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = j + F1 * r;
+            if (r < KS / F1) row[k] = X[q][r];                               // X_p[kx], kx = k
+            if (r == 0 && j == 0) row[KS] = X[q][r];                          // X_p[L - 0]
+            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];                  // X_p[L/2]
+            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
+        }
+    }
+    __syncthreads();
+    // Nyquist column kx = L/2 first, by wave 0 (a wave-uniform branch: lane-divergent code costs the
+    // register allocator dearly) in its own exchange areas while the other waves gather.  Its four
+    // lines compute the same column and store the same values.  The rows' bins are real (Re / Im of
+    // the pair's X_p[L/2]); columns 0 and L/2 keep real parts only (self-conjugate row bins, as irfft).
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
+        float2 D[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int y = j + F1 * s;
+            const float2 w = nyq[y >> 1];
+            D[s] = make_float2((y & 1) ? w.y : w.x, 0.f);
+        }
+        fused_column<L, FIRST, LAST>(a, D, g, L / 2, j, xnyq + line * FG::XCH, tw, r1, r2, r2n);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = D[s].x;  // read back in phase I
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");  // keep the gather below the Nyquist column (register pressure)
+    float2 C[F2];
+    fused_gather<L>(S, line, j, C);
+    __syncthreads();  // S -> exchange areas
+    fused_column<L, FIRST, LAST>(a, C, g, line, j, my, tw, r1, r2, r2n);
+    if constexpr (GD_FUSED_PARK & 2) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) park1[s * FG::THREADS + tid] = C[s];
+    }
+    __syncthreads();  // exchange areas -> slice B
+
+    // B: columns KS..2KS-1, bins parked in the output image
+    if constexpr (GD_FUSED_PARK & 1) {
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q)
+#pragma unroll
+            for (int r = RB0; r < RB1; ++r) X[q][r] = park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + opaque(tid)];
+    }
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        float2* row = S + (line + LINES * q) * SLD;
+#pragma unroll
+        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
+            const int k = j + F1 * r;
+            if (r < 2 * KS / F1) row[k - KS] = X[q][r];                       // X_p[kx], kx = k
+            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
+                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];        // X_p[L - kx] at KS + (kx - KS)
+            }
+        }
+    }
+    __syncthreads();
+    float2 Cb[F2];
+    fused_gather<L>(S, line, j, Cb);
+    __syncthreads();
+    fused_column<L, FIRST, LAST>(a, Cb, g, KS + line, j, my, tw, r1, r2, r2n);
+
+    // I: rows [hf L/2, (hf+1) L/2)
+    float* out = a.o0 + (size_t)g * L * L;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        __syncthreads();  // exchange areas / previous half's reads -> row half spectra
+#pragma unroll
+        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
+            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
+            float2 c;
+            if constexpr (GD_FUSED_PARK & 2) c = park1[s * FG::THREADS + opaque(tid)];
+            else c = C[s];
+            rr[line] = make_float2(c.x, line == 0 ? 0.f : c.y);  // column 0: real part (irfft)
+            rr[KS + line] = Cb[s];
+        }
+        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        __syncthreads();
+        float2 V[F2];
+        const int jj = opaque(j);
+        const float2* re = S + (2 * opaque(line)) * SLD;
+        const float2* ro = re + SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = jj + F1 * r;
+            float2 be, bo;
+            if (k <= L / 2) {
+                be = re[k];
+                bo = ro[k];
+            } else {
+                be = cconj(re[L - k]);
+                bo = cconj(ro[L - k]);
+            }
+            V[r] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+        __syncthreads();  // row half spectra -> exchange areas
+        line_fft<L, true, true>(V, j, my, tw);
+        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            o[F1 * r] = V[r].x;
+            o[L + F1 * r] = V[r].y;
         }
     }
 }
@@ -658,6 +894,7 @@ constexpr const char* kRowFwdName = "k_row_fwd";
 constexpr const char* kColName = "k_col";
 constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
+constexpr const char* kGalIterName = "k_gal_iter";
 
 inline int fail(int code, const char* msg) {
     g_last_error = msg;
@@ -750,6 +987,16 @@ struct Launcher {
         hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid<RiTraits<MODE>::NI>(a.N)), dim3(RowGeo<L, RiTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_inv");
     }
+    template <bool FIRST, bool LAST>
+    static int gal_iter_v(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalIterName, FIRST + 2 * LAST), st);
+        hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_iter");
+    }
+    static int gal_iter(const Args& a, hipStream_t st) {
+        if (a.first) return a.last ? gal_iter_v<true, true>(a, st) : gal_iter_v<true, false>(a, st);
+        return a.last ? gal_iter_v<false, true>(a, st) : gal_iter_v<false, false>(a, st);
+    }
     template <int MODE>
     static int rif(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kRowInvFwdName, MODE), st);
@@ -775,6 +1022,7 @@ struct Launcher {
 size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk; 0 = one pass
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
+int g_fused = 1;  // Gaussian iterations through k_gal_iter where a size has it
 
 struct PipeRes {
     bool ok = false;
@@ -801,6 +1049,9 @@ inline PipeRes* pipe_res() {
     return &r;
 }
 
+template <int L>
+constexpr bool has_fused() { return L == 256; }
+
 inline Args offset_args(const Args& a, int g0, int n, int L) {
     Args b = a;
     b.N = n;
@@ -812,7 +1063,6 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
     if (b.s_u1) b.s_u1 += spec;
     if (b.s_w) b.s_w += spec;
     if (b.Tw) b.Tw += 2 * spec;   // full-batch workspace layouts [N][2][K][L]
-    if (b.Tx0) b.Tx0 += 2 * spec;
     if (b.y) b.y += img;
     if (b.a0) b.a0 += img;
     if (b.a1) b.a1 += img;
@@ -897,29 +1147,29 @@ struct Ops {
         });
     }
     static int admm_init_gauss(Args a0, hipStream_t st0) {
-        // Gaussian state |H|^2, G; x0 -> zin (a.o2); x0's row spectra -> slot 1 of the FULL workspace
-        // where iteration 0 picks them up (Tx0), whatever the chunking
-        a0.Tw = nullptr;
-        a0.Tx0 = a0.T;  // full-batch workspace, offset per chunk
+        // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
-            b.Tx0 = nullptr;
             GD_TRY(Lc::template rf<RF_YA>(b, st));
             GD_TRY(Lc::template col<C_G_INIT>(b, st));
-            b.o0 = a.o2;   // RIF_CLAMP writes x0 -> zin
-            b.Tw = a.Tx0;  // ... and its row spectra to slot 1 of the full-batch workspace
+            b.o0 = a.o2;    // RIF_CLAMP writes x0 -> zin and its row spectra -> slot 1
             b.t_slot = 1;
-            return Lc::template rif<RIF_CLAMP>(b, st);
+            GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
+            return Lc::template col<C_G_W1>(b, st);
         });
     }
-    static int admm_iter_gauss(Args a0, hipStream_t st0) {
+    static int admm_iter_gauss(Args a, hipStream_t st0) {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
-        a0.Tw = nullptr;
-        a0.Tx0 = a0.first ? a0.T : nullptr;  // x0 spectra left by admm_init_gauss (full-batch layout)
-        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
-            GD_TRY(Lc::template rf<RF_ONE>(a, st));
-            GD_TRY(a.first ? Lc::template col<C_G_ITER0>(a, st) : Lc::template col<C_G_ITER>(a, st));
-            return Lc::template ri<RI_OUT1>(a, st);
+        if constexpr (has_fused<L>()) {
+            if (g_fused) return Lc::gal_iter(a, st0);  // one pass, no workspace
+        }
+        return for_chunks(a, L, st0, [&](const Args& b, hipStream_t st) {
+            GD_TRY(Lc::template rf<RF_ONE>(b, st));
+            if (b.first)
+                GD_TRY(b.last ? Lc::template col<C_G_ITER_FL>(b, st) : Lc::template col<C_G_ITER_F>(b, st));
+            else
+                GD_TRY(b.last ? Lc::template col<C_G_ITER_L>(b, st) : Lc::template col<C_G_ITER>(b, st));
+            return Lc::template ri<RI_OUT1>(b, st);
         });
     }
     static int admm_iter(Args a0, hipStream_t st0) {
@@ -1007,7 +1257,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.7-pipelined"; }
+const char* gd_engine_rev(void) { return "r01.8"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -1220,6 +1470,12 @@ size_t gd_set_chunk_bytes(size_t bytes) {
 int gd_set_pipeline_streams(int streams) {
     const int old = g_pipe_streams;
     if (streams >= 1) g_pipe_streams = streams < kMaxPipe ? streams : kMaxPipe;
+    return old;
+}
+
+int gd_set_fused_iteration(int on) {
+    const int old = g_fused;
+    g_fused = on ? 1 : 0;
     return old;
 }
 

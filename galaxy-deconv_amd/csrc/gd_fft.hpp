@@ -57,6 +57,7 @@ __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
     return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
 }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
@@ -194,17 +195,40 @@ __device__ __forceinline__ void fill_twiddles(float2* tw, int tid, int nthreads)
 
 // Length-L FFT over the F1 lanes of a line.  v[r] = x[j + F1*r] in, X[j + F1*r] out.
 // xch: this line's private LDS exchange area (xch_elems<L>() float2); tw: twiddle table.
-template <int L, bool INV>
+// LEAN (F2 = 16 only): the 15 twiddles W^{j k1} come from 6 table entries, W^{j (a + 4b)} =
+// W^{4jb} W^{ja} (one extra rounding on 9 of them), so a line needs 12 twiddle registers instead
+// of 30 - for kernels that run at the 128-VGPR budget of 1024-thread workgroups.
+template <int L, bool INV, bool LEAN = false>
 __device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2* xch, const float2* tw) {
     constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, M = F2 / F1, LD = F2 + 1;
     static_assert(F2 % F1 == 0, "line plan needs F1 | F2");
+    static_assert(!LEAN || F2 == 16, "lean twiddles are for 16 points per lane");
     // stage A: DFT-F2 over n2 (lane j = n1), then twiddle W_L^{n1 k1}
     DFT<F2, INV>::run(v);
+    if constexpr (LEAN) {
+        float2 t1[4], t4[4];
 #pragma unroll
-    for (int k1 = 1; k1 < F2; ++k1) {
-        float2 w = tw[j * k1];  // j*k1 <= (F1-1)(F2-1) < L: no wrap
-        if (INV) w.y = -w.y;
-        v[k1] = cmul(v[k1], w);
+        for (int i = 1; i < 4; ++i) {
+            t1[i] = tw[j * i];
+            t4[i] = tw[4 * j * i];
+            if (INV) {
+                t1[i].y = -t1[i].y;
+                t4[i].y = -t4[i].y;
+            }
+        }
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            const int a = k1 & 3, b = k1 >> 2;
+            const float2 w = a == 0 ? t4[b] : (b == 0 ? t1[a] : cmul(t4[b], t1[a]));
+            v[k1] = cmul(v[k1], w);
+        }
+    } else {
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            float2 w = tw[j * k1];  // j*k1 <= (F1-1)(F2-1) < L: no wrap
+            if (INV) w.y = -w.y;
+            v[k1] = cmul(v[k1], w);
+        }
     }
 #pragma unroll
     for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v[k1];

@@ -112,6 +112,12 @@ int gd_subnet_features(const void* otf128_half, const float* params, float* feat
 size_t gd_set_chunk_bytes(size_t bytes);
 int gd_set_pipeline_streams(int streams);
 
+/* Fused Gaussian iteration: at sizes that have it (256^2) gd_admm_iter runs ONE kernel per call, one
+ * workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic); on = 0 selects the
+ * three-kernel path (row pass / column pass / row pass through the workspace).  Returns the previous
+ * setting; process-wide. */
+int gd_set_fused_iteration(int on);
+
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,
  * the SubNet kernel) on the caller's stream; level 2 also brackets every kernel launch on its own
  * stream (adds two event records per launch - under pipelining that perturbs what it measures).

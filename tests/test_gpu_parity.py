@@ -117,14 +117,51 @@ def _spectral_model(n, llh, dev, rho1, rho2):
     return m
 
 
+@pytest.fixture(params=[1, 0], ids=["fused", "three_kernel"])
+def fused(request):
+    """Gaussian iterations through the one-kernel whole-galaxy path (256^2) or the three-kernel path."""
+    from gdeconv import _lib
+    lib = _lib.load()
+    old = lib.gd_set_fused_iteration(request.param)
+    yield request.param
+    lib.gd_set_fused_iteration(old)
+
+
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
-def test_admm256_spectral_engine(dev, llh):
+def test_admm256_spectral_engine(dev, llh, fused):
     g = golden("admm256_id.npz")
     obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
     m = _spectral_model(8, llh, dev, T(g[f"{llh}_rho1"]), T(g[f"{llh}_rho2"]))
     with torch.no_grad():
         out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
     assert nerr(out, T(g[f"{llh}_out"])) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_fused_iteration_matches_three_kernel_path(dev, n):
+    """k_gal_iter (first / middle / last variants) against the three-kernel path and the oracle, with
+    per-galaxy rho and a ragged batch."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 37
+    obs, psf, alpha, _ = make_batch(N, 256, seed=40 + n, device=dev)
+    gen = torch.Generator().manual_seed(n)
+    rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
+    old = lib.gd_set_fused_iteration(1)
+    try:
+        with torch.no_grad():
+            out_f = m(obs, psf, alpha).cpu()
+            lib.gd_set_fused_iteration(0)
+            out_t = m(obs, psf, alpha).cpu()
+    finally:
+        lib.gd_set_fused_iteration(old)
+    assert nerr(out_f, out_t) < 2e-6
+    idx = [0, 17, 36]
+    ref = O.admm_forward(obs[idx].cpu(), psf[idx].cpu(), alpha[idx].cpu(), rho1[idx].cpu(), rho2[idx].cpu())
+    assert nerr(out_f[idx], ref) < TOL
 
 
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
@@ -224,7 +261,7 @@ def test_errors_are_loud(eng, dev):
 
 
 # ------------------------------------------------------------------ full-size properties (BASELINE sizes)
-def test_full_batch_invariance_and_sharding(dev):
+def test_full_batch_invariance_and_sharding(dev, fused):
     """4096 x 256^2 (configs[2]): every galaxy's result is independent of the batch it rides in
     (bit-exact), so contiguous batch shards (the multi-GPU split) reproduce the full batch."""
     from gdeconv.synth import make_batch

@@ -18,10 +18,11 @@ import re
 MODE_NAMES = {
     "k_row_fwd": ["ITER", "PSF_Y", "PSF_YP", "PSF_RAW", "PSF", "ONE", "TWO", "YA"],
     "k_col": ["ITER", "OTF_INIT", "OTF_CONV", "WIENER", "OTF", "CONV", "CONVC", "CONV2", "FWD", "INV",
-              "G_INIT", "G_ITER", "G_ITER0"],
+              "G_INIT", "G_ITER", "G_W1", "G_ITER_F", "G_ITER_L", "G_ITER_FL"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES"],
+    "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
 }
 
 
@@ -76,7 +77,8 @@ def main():
                              "hbm_bytes_per_launch": rd + wr, "launches": nf.get(k, 0)}
     # whole Gaussian ADMM iteration (RF(z) -> C_G_ITER[0] -> RI(zin), all chunks): traffic per call
     L = a.size
-    members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER0>", f"k_row_inv<{L},OUT1>"]
+    members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER_F>", f"k_col<{L},G_ITER_L>",
+               f"k_row_inv<{L},OUT1>", f"k_gal_iter<{L},MID>", f"k_gal_iter<{L},FIRST>", f"k_gal_iter<{L},LAST>"]
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in out["kernels"].items() if k in members)
     if tot:
         out["kernels"][f"op_admm_iter<{L},Gaussian>"] = {
