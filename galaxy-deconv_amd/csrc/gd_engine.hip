@@ -502,19 +502,17 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 
 // ---------------------------------------------------------------- fused whole-galaxy Gaussian iteration
 // One 1024-thread workgroup per galaxy, one workgroup per CU: the galaxy's half spectrum (264 KiB at
-// 256^2) lives in that CU's registers and LDS for the whole iteration, so the row spectra never go
-// to HBM.  z -> zin moves z, zin and the state (|H|^2, G, U1, W~ read; U1, W~ written): 7.5 fp32
-// words per pixel instead of the three-kernel path's 11.6.  Phases (S = LDS union):
-//   R  64 lines x L/(2*64) row pairs (rows 2p + i 2p+1): row FFT in registers
-//   A  the bins that columns 0..L/4-1 need (X_p[kx], X_p[L-kx]) -> S; column kx = line: gather the
-//      two rows' half spectra (split of the packed pair), column FFT, spectral update, column IFFT;
-//      line 0 also does the Nyquist column kx = L/2 (its bins wait in `nyq`); results stay in registers
-//   B  the same for columns L/4..L/2-1, whose bins waited in registers
-//   I  per half of the rows: column results -> S as row half spectra, row IFFT of the packed pairs,
-//      store (x for the last iteration, else zin = x + u1)
-#ifndef GD_FUSED_PARK
-#define GD_FUSED_PARK 3  // bit 0: park slice B's bins, bit 1: park slice A's results (see k_gal_iter)
-#endif
+// 256^2) lives in that CU's registers and LDS for the whole iteration, so no spectrum goes to HBM:
+// z -> zin moves z, zin and the state (|H|^2, G, U1, W~ read; U1, W~ written), 7.5 fp32 words per
+// pixel instead of the three-kernel path's 11.6.  Phases (S = the LDS union):
+//   R  line l transforms row pairs l and l + 64 (rows 2p + i 2p+1) in registers
+//   A  the bins that columns 0..63 need (X_p[kx], X_p[L - kx]) -> S; line kx gathers its column (the
+//      two rows' half spectra split out of the packed pair); then columns 64..127's bins -> S while
+//      column A is transformed (register-only FFT: S is occupied), updated and transformed back.
+//      Columns 0 and L/2 are real over the rows and ride together in line 0 (see below).
+//   B  gather columns 64..127 from S; column A's results -> S in row layout; column B as column A
+//   I  per half of the rows: column B's results -> S beside column A's (whose other half waits in
+//      registers), row IFFT of the packed pairs, store (x on the last iteration, else zin = x + u1)
 #ifndef GD_FUSED_FFTBAR
 #define GD_FUSED_FFTBAR 1
 #endif
@@ -522,11 +520,21 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #define GD_FUSED_GROUP 4
 #endif
 // A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
-// (and kept live from) an earlier phase's identical computation.
+// (and kept live from) an earlier phase's identical computation (register budget: 128 VGPRs at
+// 1024 threads).
 __device__ __forceinline__ int opaque(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+
+// Optional per-workgroup phase timestamps (tools/kbench_fused.hip builds with GD_FUSED_TRACE=1).
+#if GD_FUSED_TRACE
+__device__ unsigned long long* g_fused_trace;
+#define GD_TRACE(k)                                                                                   \
+    if (tid == 0) g_fused_trace[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define GD_TRACE(k)
+#endif
 
 template <int L>
 struct FusedGeo {
@@ -534,13 +542,14 @@ struct FusedGeo {
     static constexpr int THREADS = 1024, LINES = THREADS / F1;
     static constexpr int NP = L / 2, PPL = NP / LINES;  // row pairs; pairs per line
     static constexpr int KS = L / 4;                    // columns per slice (one per line)
-    static constexpr int SLD = 2 * KS + 4;              // S row stride (float2), >= K, 8 dwords mod 64 banks
+    static constexpr int SLD = 2 * KS + 4;              // slice layout [pair][SLD]: X_p[kx], X_p[L-kx]
+    static constexpr int ALD = KS + 2;                  // row layout [row][ALD]: one slice's columns
     static constexpr int XCH = xch_elems<L>();
-    static constexpr int U = cmax(NP * SLD, LINES * XCH);
+    static constexpr int U = cmax(cmax(NP * SLD, L * ALD), LINES * XCH);
     static_assert(LINES == KS, "one column per line and slice");
     static_assert(NP == 2 * LINES && PPL == 2, "two row pairs per line; half the rows per inverse pass");
     static_assert(KS % F1 == 0 && (L / 2) % F1 == 0, "slice edges on lane-register boundaries");
-    static_assert(SLD >= K, "row half spectrum must fit a stride");
+    static_assert(L <= THREADS && (NP * KS) % THREADS == 0, "Nyquist column: one element per thread");
 };
 
 // Column c of a slice from S = [pair][SLD] holding X_p[kx] at [c] and X_p[(L - kx) mod L] at [KS + c]:
@@ -559,14 +568,14 @@ __device__ __forceinline__ void fused_gather(const float2* S, int c, int j, floa
     }
 }
 
+// Spectral update of column kx (rows ky = j + F1 s of this lane).
 template <int L, bool FIRST, bool LAST>
-__device__ __forceinline__ void fused_column(const Args& a, float2 (&C)[FusedGeo<L>::F2], int g, int kx, int j,
-                                             float2* my, const float2* tw, float r1, float r2, float r2n) {
+__device__ __forceinline__ void fused_update(const Args& a, float2 (&C)[FusedGeo<L>::F2], int g, int kx, int j,
+                                             float r1, float r2, float r2n) {
     using FG = FusedGeo<L>;
     constexpr float inv_n = float(1.0 / double(L * L));
     j = opaque(j);
     kx = opaque(kx);
-    line_fft<L, false, true>(C, j, my, tw);
 #if GD_FUSED_FFTBAR
     __builtin_amdgcn_sched_barrier(0);  // keep the state loads below the FFT (register pressure)
 #endif
@@ -576,55 +585,66 @@ __device__ __forceinline__ void fused_column(const Args& a, float2 (&C)[FusedGeo
         C[s] = gauss_iter_elem<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
         if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
     }
-    line_fft<L, true, true>(C, j, my, tw);
+}
+
+// Workgroup barrier that orders LDS only: outstanding global loads and stores stay in flight
+// (__syncthreads would drain them at every phase boundary).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 template <int L, bool FIRST, bool LAST>
 __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, ALD = FG::ALD, LINES = FG::LINES;
+    constexpr float inv_n = float(1.0 / double(L * L));
     __shared__ float2 tw[L];
     __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];
-    __shared__ float2 xnyq[64 / F1 * FG::XCH];  // wave 0's exchange areas for the Nyquist column
-    __shared__ float nyqo[L];         // ... and its result (real parts)
+    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
+    __shared__ float nyqo[L];       // x(., L/2)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
+    const bool l0 = (line == 0);
     float2* my = S + line * FG::XCH;
     fill_twiddles<L>(tw, tid, FG::THREADS);
     const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    GD_TRACE(0);
 
     // R: pair p = line + LINES q
     float2 X[FG::PPL][F2];
-    const float* z = a.a0 + (size_t)g * L * L;
+    {
+        const float* z = a.a0 + (size_t)g * L * L;
 #pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+        for (int q = 0; q < FG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
 #pragma unroll
-        for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+        }
     }
-    __syncthreads();  // twiddles
+    __syncthreads();  // twiddles; all of z loaded (zin may alias z: the park stores below write it)
+    GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
     // Register budget (128 VGPRs at 1024 threads): what a later phase needs but the current one does
-    // not is parked in this galaxy's output image, written whole at the end (z is already in registers,
-    // so zin == z is fine): region 0 = slice B's bins (registers r in [RB0, RB1), the few at RB1 stay),
-    // region 1 = slice A's column results.  Lane-contiguous (512 B per wave instruction), read back
-    // by the same thread; region 0 is consumed before phase I writes rows 0..L/2-1 over it, and each
-    // half of region 1 before phase I writes rows L/2..L-1.
+    // not is parked in this galaxy's output image, written whole at the end: region 0 = slice B's
+    // bins (registers r in [RB0, RB1); the few at RB1 stay), region 1 = column A's results.
+    // Lane-contiguous (512 B per wave instruction), read back by the same thread; every parked value
+    // is read back (and consumed into LDS) before phase I writes that part of the image.
     float2* park0 = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L);
     float2* park1 = park0 + (size_t)L * L / 4;
     constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
     static_assert(FG::PPL * (RB1 - RB0) * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4, "park regions");
-    if constexpr (GD_FUSED_PARK & 1) {
 #pragma unroll
-        for (int q = 0; q < FG::PPL; ++q)
+    for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-            for (int r = RB0; r < RB1; ++r) park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + tid] = X[q][r];
-    }
-    __syncthreads();  // exchange areas -> slice A
+        for (int r = RB0; r < RB1; ++r) park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + tid] = X[q][r];
+    lds_barrier();  // exchange areas -> slice A
+    GD_TRACE(2);
 
-    // A: columns 0..KS-1 (+ Nyquist)
+    // A: bins of columns 0..KS-1 and the Nyquist bins
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
         const int p = line + LINES * q;
@@ -638,42 +658,64 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
             if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
         }
     }
-    __syncthreads();
-    // Nyquist column kx = L/2 first, by wave 0 (a wave-uniform branch: lane-divergent code costs the
-    // register allocator dearly) in its own exchange areas while the other waves gather.  Its four
-    // lines compute the same column and store the same values.  The rows' bins are real (Re / Im of
-    // the pair's X_p[L/2]); columns 0 and L/2 keep real parts only (self-conjugate row bins, as irfft).
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {
-        float2 D[F2];
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int y = j + F1 * s;
-            const float2 w = nyq[y >> 1];
-            D[s] = make_float2((y & 1) ? w.y : w.x, 0.f);
-        }
-        fused_column<L, FIRST, LAST>(a, D, g, L / 2, j, xnyq + line * FG::XCH, tw, r1, r2, r2n);
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = D[s].x;  // read back in phase I
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");  // keep the gather below the Nyquist column (register pressure)
+    lds_barrier();
+    GD_TRACE(3);
+    // Columns 0 and L/2 are real sequences over the rows (Re / Im of the pairs' X_p[0], X_p[L/2]):
+    // line 0 carries both as one complex column Z = c_0 + i c_{L/2}, splits the spectra after the
+    // forward FFT (C_0 = (Z + conj Z(-ky))/2, C_{L/2} = (Z - conj Z(-ky))/2i), updates column 0 itself
+    // and hands column L/2 to the first L/64 waves, one element per thread; the results are packed
+    // back the same way, so the inverse FFT's real / imaginary parts are x(., 0) and x(., L/2) (only
+    // real parts are kept for the self-conjugate row bins, as irfft does).
     float2 C[F2];
     fused_gather<L>(S, line, j, C);
-    __syncthreads();  // S -> exchange areas
-    fused_column<L, FIRST, LAST>(a, C, g, line, j, my, tw, r1, r2, r2n);
-    if constexpr (GD_FUSED_PARK & 2) {
 #pragma unroll
-        for (int s = 0; s < F2; ++s) park1[s * FG::THREADS + tid] = C[s];
+    for (int s = 0; s < F2; ++s) {
+        const int y = j + F1 * s;
+        const float2 w = nyq[y >> 1];
+        if (l0) C[s].y = (y & 1) ? w.y : w.x;
     }
-    __syncthreads();  // exchange areas -> slice B
+    lds_barrier();  // S -> exchange areas
+    GD_TRACE(4);
+    line_fft<L, false, true>(C, opaque(j), my, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) my[j + F1 * s] = C[s];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int ky = j + F1 * s;
+            const float2 z = C[s], zm = my[(L - ky) & (L - 1)];
+            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        }
+        wave_lds_sync();  // (the inverse FFT rewrites the exchange area)
+    }
+    lds_barrier();  // nyqc complete
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
+        nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
+                                                 true, inv_n);
+    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n);
+    lds_barrier();  // Nyquist results
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const float2 cn = nyqc[j + F1 * s];
+        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
+    }
+    line_fft<L, true, true>(C, opaque(j), my, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
+    }
+#pragma unroll
+    for (int s = 0; s < F2; ++s) park1[s * FG::THREADS + tid] = C[s];
+    lds_barrier();  // exchange areas -> slice B
+    GD_TRACE(5);
 
-    // B: columns KS..2KS-1, bins parked in the output image
-    if constexpr (GD_FUSED_PARK & 1) {
+    // B: columns KS..2KS-1
 #pragma unroll
-        for (int q = 0; q < FG::PPL; ++q)
+    for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-            for (int r = RB0; r < RB1; ++r) X[q][r] = park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + opaque(tid)];
-    }
+        for (int r = RB0; r < RB1; ++r) X[q][r] = park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + opaque(tid)];
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
         float2* row = S + (line + LINES * q) * SLD;
@@ -686,46 +728,51 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
+    GD_TRACE(6);
     float2 Cb[F2];
     fused_gather<L>(S, line, j, Cb);
-    __syncthreads();
-    fused_column<L, FIRST, LAST>(a, Cb, g, KS + line, j, my, tw, r1, r2, r2n);
+    lds_barrier();
+    GD_TRACE(7);
+    line_fft<L, false, true>(Cb, opaque(j), my, tw);
+    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n);
+    line_fft<L, true, true>(Cb, opaque(j), my, tw);
 
-    // I: rows [hf L/2, (hf+1) L/2)
+    // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
+    // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
     float* out = a.o0 + (size_t)g * L * L;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-        __syncthreads();  // exchange areas / previous half's reads -> row half spectra
+        lds_barrier();  // exchange areas -> row half spectra
 #pragma unroll
         for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
             float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
-            float2 c;
-            if constexpr (GD_FUSED_PARK & 2) c = park1[s * FG::THREADS + opaque(tid)];
-            else c = C[s];
-            rr[line] = make_float2(c.x, line == 0 ? 0.f : c.y);  // column 0: real part (irfft)
+            const float2 c = park1[s * FG::THREADS + opaque(tid)];
+            rr[line] = make_float2(c.x, l0 ? 0.f : c.y);  // column 0: real part (irfft)
             rr[KS + line] = Cb[s];
         }
         for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        __syncthreads();
+        lds_barrier();
         float2 V[F2];
-        const int jj = opaque(j);
-        const float2* re = S + (2 * opaque(line)) * SLD;
-        const float2* ro = re + SLD;
+        {
+            const int jj = opaque(j);
+            const float2* re = S + (2 * opaque(line)) * SLD;
+            const float2* ro = re + SLD;
 #pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            const int k = jj + F1 * r;
-            float2 be, bo;
-            if (k <= L / 2) {
-                be = re[k];
-                bo = ro[k];
-            } else {
-                be = cconj(re[L - k]);
-                bo = cconj(ro[L - k]);
+            for (int r = 0; r < F2; ++r) {
+                const int k = jj + F1 * r;
+                float2 be, bo;
+                if (k <= L / 2) {
+                    be = re[k];
+                    bo = ro[k];
+                } else {
+                    be = cconj(re[L - k]);
+                    bo = cconj(ro[L - k]);
+                }
+                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
             }
-            V[r] = make_float2(be.x - bo.y, be.y + bo.x);
         }
-        __syncthreads();  // row half spectra -> exchange areas
+        lds_barrier();  // row half spectra -> exchange areas
         line_fft<L, true, true>(V, j, my, tw);
         float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
 #pragma unroll
@@ -733,6 +780,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
             o[F1 * r] = V[r].x;
             o[L + F1 * r] = V[r].y;
         }
+        GD_TRACE(8 + hf);
     }
 }
 

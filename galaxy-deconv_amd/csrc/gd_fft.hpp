@@ -195,14 +195,69 @@ __device__ __forceinline__ void fill_twiddles(float2* tw, int tid, int nthreads)
 
 // Length-L FFT over the F1 lanes of a line.  v[r] = x[j + F1*r] in, X[j + F1*r] out.
 // xch: this line's private LDS exchange area (xch_elems<L>() float2); tw: twiddle table.
+// Register-only 16 x 16 transpose across the 16 lanes of a line (F1 = F2 = 16): lane j holds v[k]
+// = x_j[k] on entry and v[n] = x_n[j] on exit.  The register index a lane needs depends on the lane,
+// so the data are rotated by the lane index (four conditional stages of v_cndmask), moved with DPP
+// row rotations (uniform register index), and rotated back.  No LDS: for kernels whose LDS is
+// occupied by data while they transform.
+#ifndef GD_DPP_ROR_DIR
+#define GD_DPP_ROR_DIR 1  // row_ror:r delivers lane (j - r) mod 16 to lane j
+#endif
+template <int R>
+__device__ __forceinline__ float dpp_row_ror(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + R, 0xF, 0xF, false));
+}
+template <int SGN, int B = 0>
+__device__ __forceinline__ void lane_rotate16(float2 (&x)[16], int j) {  // x[k] <- x[(k + SGN j) mod 16]
+    if constexpr (B < 4) {  // stage B: rotate by 2^B where bit B of j is set (compile-time indices)
+        constexpr int d = 1 << B;
+        const bool c = (j >> B) & 1;
+        float2 t[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            // values made opaque first: a select of two array elements would otherwise be folded into
+            // a load from a selected address, i.e. a dynamically indexed array in scratch memory
+            float2 p = x[(k + SGN * d) & 15], q = x[k];
+            asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(q.x), "+v"(q.y));
+            t[k] = c ? p : q;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = t[k];
+        lane_rotate16<SGN, B + 1>(x, j);
+    }
+}
+// rounds R..15 of the transpose (forceinline recursion, not a lambda: arrays must stay in registers)
+template <int R>
+__device__ __forceinline__ void dpp_rounds(float2 (&z)[16], const float2 (&v)[16]) {
+    if constexpr (R < 16) {
+        constexpr int src = GD_DPP_ROR_DIR > 0 ? R : (16 - R) & 15;
+        z[R] = make_float2(dpp_row_ror<R>(v[src].x), dpp_row_ror<R>(v[src].y));
+        dpp_rounds<R + 1>(z, v);
+    }
+}
+__device__ __forceinline__ void transpose16_dpp(float2 (&v)[16], int j) {
+    // w[c] = v[(c + j) mod 16]: round r then moves, with ONE register index for all lanes, element
+    // j of lane j -/+ r (row_ror direction GD_DPP_ROR_DIR = +1 / -1)
+    lane_rotate16<1>(v, j);
+    float2 z[16];
+    z[0] = v[0];
+    dpp_rounds<1>(z, v);
+    // z[r] holds lane n1 = j -/+ r; want v[n1] = z[(+/-(j - n1)) mod 16]
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = z[GD_DPP_ROR_DIR > 0 ? (16 - m) & 15 : m];
+    lane_rotate16<-1>(v, j);
+}
+
 // LEAN (F2 = 16 only): the 15 twiddles W^{j k1} come from 6 table entries, W^{j (a + 4b)} =
 // W^{4jb} W^{ja} (one extra rounding on 9 of them), so a line needs 12 twiddle registers instead
 // of 30 - for kernels that run at the 128-VGPR budget of 1024-thread workgroups.
-template <int L, bool INV, bool LEAN = false>
+// DPP: register transpose (transpose16_dpp) instead of the LDS exchange (xch unused), F1 = F2 = 16.
+template <int L, bool INV, bool LEAN = false, bool DPP = false>
 __device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2* xch, const float2* tw) {
     constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, M = F2 / F1, LD = F2 + 1;
     static_assert(F2 % F1 == 0, "line plan needs F1 | F2");
     static_assert(!LEAN || F2 == 16, "lean twiddles are for 16 points per lane");
+    static_assert(!DPP || (F1 == 16 && F2 == 16), "register transpose is for 16 x 16 lines");
     // stage A: DFT-F2 over n2 (lane j = n1), then twiddle W_L^{n1 k1}
     DFT<F2, INV>::run(v);
     if constexpr (LEAN) {
@@ -229,6 +284,11 @@ __device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2
             if (INV) w.y = -w.y;
             v[k1] = cmul(v[k1], w);
         }
+    }
+    if constexpr (DPP) {
+        transpose16_dpp(v, j);  // lane j: v[n1] = (element k1 = j of lane n1)
+        DFT<F1, INV>::run(v);   // lane j holds X[j + F1 k2] in v[k2]
+        return;
     }
 #pragma unroll
     for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v[k1];
