@@ -516,6 +516,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #ifndef GD_FUSED_FFTBAR
 #define GD_FUSED_FFTBAR 1
 #endif
+#ifndef GD_FUSED_NPB
+#define GD_FUSED_NPB 8  // slice-B bin registers (of 8) parked in global memory during column A (fewer: spills)
+#endif
 #ifndef GD_FUSED_GROUP
 #define GD_FUSED_GROUP 4
 #endif
@@ -628,19 +631,22 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
-    // Register budget (128 VGPRs at 1024 threads): what a later phase needs but the current one does
-    // not is parked in this galaxy's output image, written whole at the end: region 0 = slice B's
-    // bins (registers r in [RB0, RB1); the few at RB1 stay), region 1 = column A's results.
-    // Lane-contiguous (512 B per wave instruction), read back by the same thread; every parked value
-    // is read back (and consumed into LDS) before phase I writes that part of the image.
+    // Register budget (128 VGPRs at 1024 threads; a column's FFTs and update take ~92): what a later
+    // phase needs beyond that is parked in this galaxy's output image, written whole at the end:
+    // region 0 = part of slice B's bins (registers r in [RB0, RB0 + NPB)), region 1 = column A's
+    // results.  Lane-contiguous (512 B per wave instruction),
+    // read back by the same thread; every parked value is read back (and consumed into LDS) before
+    // phase I writes that part of the image.
     float2* park0 = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L);
     float2* park1 = park0 + (size_t)L * L / 4;
     constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
-    static_assert(FG::PPL * (RB1 - RB0) * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4, "park regions");
+    constexpr int NPB = GD_FUSED_NPB;                   // of which parked
+    static_assert(NPB <= RB1 - RB0 && FG::PPL * NPB * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4,
+                  "park regions");
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-        for (int r = RB0; r < RB1; ++r) park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + tid] = X[q][r];
+        for (int r = RB0; r < RB0 + NPB; ++r) park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
     lds_barrier();  // exchange areas -> slice A
     GD_TRACE(2);
 
@@ -715,7 +721,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-        for (int r = RB0; r < RB1; ++r) X[q][r] = park0[(q * (RB1 - RB0) + r - RB0) * FG::THREADS + opaque(tid)];
+        for (int r = RB0; r < RB0 + NPB; ++r) X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
         float2* row = S + (line + LINES * q) * SLD;
@@ -741,8 +747,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
     // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
     float* out = a.o0 + (size_t)g * L * L;
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
+    static_for<0, 2>([&](auto hfc) {
+        constexpr int hf = decltype(hfc)::value;
         lds_barrier();  // exchange areas -> row half spectra
 #pragma unroll
         for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
@@ -781,7 +787,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
             o[L + F1 * r] = V[r].y;
         }
         GD_TRACE(8 + hf);
-    }
+    });
 }
 
 // ---------------------------------------------------------------- RI: row inverse + sink
