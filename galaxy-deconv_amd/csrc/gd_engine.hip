@@ -75,11 +75,14 @@ struct Args {
     float2* s_w;           //   conj(H) F(v - u2)
     int t_slot;            // image slot of T that row-forward kernels write (RIF_CLAMP -> 1)
     float2* Tw;            // if set: row-forward kernels write here (full-batch layout) instead of T
+    const float* ltl;      // Tikhonov |L|^2 half spectrum [*][K][L] (nullptr: filter 'Identity')
+    long long ltl_gstride; // elements between galaxies' |L|^2 (0 = one shared filter)
 };
 
-enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA };
+enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR };
 enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV,
-               C_G_INIT, C_G_ITER, C_G_W1, C_G_ITER_F, C_G_ITER_L, C_G_ITER_FL };  // _F first, _L last iteration
+               C_G_INIT, C_G_ITER, C_G_W1, C_G_ITER_F, C_G_ITER_L, C_G_ITER_FL,  // _F first, _L last iteration
+               C_TIKHONOV, C_POWER };
 enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
 enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
@@ -206,12 +209,17 @@ __device__ __forceinline__ float4 rf_source4(const Args& a, int g, int im, int r
             return make_float4(z.x - u.x, z.y - u.y, z.z - u.z, z.w - u.w);
         }
         return ld4(a.a2 + pix);                                        // w = v - u2
-    } else if constexpr (MODE == RF_PSF || MODE == RF_PSF_Y || MODE == RF_PSF_YP || MODE == RF_PSF_RAW) {
+    } else if constexpr (MODE == RF_PSF || MODE == RF_PSF_Y || MODE == RF_PSF_YP || MODE == RF_PSF_RAW ||
+                         MODE == RF_PSF_YAR) {
         if (im == 0)
             return make_float4(shifted_psf(a, g, r, c, L), shifted_psf(a, g, r, c + 1, L),
                                shifted_psf(a, g, r, c + 2, L), shifted_psf(a, g, r, c + 3, L));
         const float4 y = ld4(a.y + pix);
         if constexpr (MODE == RF_PSF_RAW) return y;
+        if constexpr (MODE == RF_PSF_YAR) {                            // y / alpha (Tikhonov: no max)
+            const float al = a.alpha(g);
+            return make_float4(y.x / al, y.y / al, y.z / al, y.w / al);
+        }
         float4 yp = make_float4(fmaxf(y.x, 0.f), fmaxf(y.y, 0.f), fmaxf(y.z, 0.f), fmaxf(y.w, 0.f));
         if constexpr (MODE == RF_PSF_YP) {
             st4(a.o0 + pix, yp);                                       // Richardson-Lucy x0 = max(y, 0)
@@ -274,9 +282,9 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI, RBX>::THREADS)) void
 template <int MODE>
 struct ColTraits {
     static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
-                                 MODE == C_WIENER || MODE == C_CONV2);
+                                 MODE == C_WIENER || MODE == C_CONV2 || MODE == C_TIKHONOV);
     static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
-    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_W1);
+    static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_W1 && MODE != C_POWER);
     static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
     static constexpr bool LOAD_OTF = (MODE == C_ITER || MODE == C_CONV || MODE == C_CONVC || MODE == C_CONV2);
     static constexpr bool FWD = (MODE != C_INV);
@@ -410,6 +418,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
     const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_INIT) ? a.alpha(g) : 1.f;
+    const float lam = (MODE == C_TIKHONOV) ? a.rho1(g) : 0.f;  // Tikhonov lambda rides in rho1
     constexpr bool giter = (MODE == C_G_ITER || MODE == C_G_ITER_F || MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
     constexpr bool gfirst = (MODE == C_G_ITER_F || MODE == C_G_ITER_FL);
     constexpr bool glast = (MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
@@ -469,6 +478,16 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float div = HtH + 350.0f / al;
             const float2 num = cmulc(Q[s], Hk);
             P[s] = cscale(make_float2(num.x / div, num.y / div), inv_n);
+        } else if constexpr (MODE == C_TIKHONOV) {
+            // models/Tikhonet.py:19-29: conj(H) F(y/alpha) / (|H|^2 + lam)        (filter 'Identity')
+            //                           conj(H) F(y/alpha) / (|H|^2 + lam |L|^2)  (filter 'Laplacian')
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float div = a.ltl ? HtH + lam * a.ltl[(size_t)g * a.ltl_gstride + (size_t)kx * L + ky] : HtH + lam;
+            const float2 num = cmulc(Q[s], Hk);
+            P[s] = cscale(make_float2(num.x / div, num.y / div), inv_n);
+        } else if constexpr (MODE == C_POWER) {
+            // |F(x)|^2 of a real filter image (the Laplacian's LtL, models/Tikhonet.py:26-27)
+            if (valid) a.s_hh[ob + ky] = P[s].x * P[s].x + P[s].y * P[s].y;
         } else if constexpr (MODE == C_OTF_CONV) {
             P[s] = cscale(cmul(Q[s], Hk), inv_n);
         } else if constexpr (MODE == C_CONV) {
@@ -1116,6 +1135,7 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
     if (b.s_g) b.s_g += spec;
     if (b.s_u1) b.s_u1 += spec;
     if (b.s_w) b.s_w += spec;
+    if (b.ltl) b.ltl += (long long)g0 * a.ltl_gstride;
     if (b.Tw) b.Tw += 2 * spec;   // full-batch workspace layouts [N][2][K][L]
     if (b.y) b.y += img;
     if (b.a0) b.a0 += img;
@@ -1240,6 +1260,17 @@ struct Ops {
             GD_TRY(Lc::template col<C_WIENER>(a, st));
             return Lc::template ri<RI_OUT1>(a, st);
         });
+    }
+    static int tikhonov(Args a0, hipStream_t st0) {
+        return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
+            GD_TRY(Lc::template rf<RF_PSF_YAR>(a, st));
+            GD_TRY(Lc::template col<C_TIKHONOV>(a, st));
+            return Lc::template ri<RI_OUT1>(a, st);
+        });
+    }
+    static int power(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_ONE>(a, st));
+        return Lc::template col<C_POWER>(a, st);
     }
     static int richardson_lucy(Args a0, int n_iters, hipStream_t st0) {
         // a.o0 = x (output, also the iterate); otf kept in a.otf.  The whole iteration loop runs per
@@ -1471,6 +1502,31 @@ int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, 
     a.otf = reinterpret_cast<float2*>(otf_half);
     a.o0 = x;
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
+}
+
+int gd_tikhonov(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+                long long alpha_stride, const float* lam, long long lam_stride, const float* ltl,
+                long long ltl_gstride, float* x, int N, int H, int W, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H));
+    if (lam == nullptr) return fail(GD_ERR_ARG, "lam required");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    a.rho1 = GalScalar{lam, lam_stride};
+    a.ltl = ltl; a.ltl_gstride = ltl_gstride;
+    a.o0 = x;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::tikhonov(a, (hipStream_t)stream); });
+}
+
+int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, H);
+    a.a0 = filt;
+    a.s_hh = power_half;
+    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::power(a, (hipStream_t)stream); });
 }
 
 int gd_profile_enable(int level) {

@@ -13,6 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before dlopen of the engin
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgdeconv.so")
 
 GD_OK = 0
+ABI_VERSION = 3
 GD_LLH = {"Gaussian": 0, "Poisson": 1}
 
 _P = ctypes.c_void_p
@@ -38,6 +39,8 @@ SIGNATURES = {
                           _P]),
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
+    "gd_tikhonov": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _P, _P]),
+    "gd_filter_power": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "gd_set_chunk_bytes": (_SZ, [_SZ]),
     "gd_set_pipeline_streams": (_I, [_I]),
     "gd_set_fused_iteration": (_I, [_I]),
@@ -69,7 +72,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.gd_abi_version() != 2:
+    if lib.gd_abi_version() != ABI_VERSION:
         raise EngineError("libgdeconv.so ABI version mismatch")
     _lib = lib
     return lib

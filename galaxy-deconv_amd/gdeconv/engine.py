@@ -159,6 +159,45 @@ def richardson_lucy(y, psf, n_iters):
     return out
 
 
+def filter_power(filt):
+    """|FFT2(filt)|^2 over the half spectrum, fp32 [N, W//2+1, H] (transposed like the OTF): the
+    Tikhonov regulariser LtL of models/Tikhonet.py:26-27 from the placed filter image."""
+    _require_device(filt)
+    lib = _lib.load()
+    f = _img(filt, "filt")
+    N, _, H, W = f.shape
+    out = torch.empty(N, W // 2 + 1, H, dtype=torch.float32, device=f.device)
+    ws = workspace(N, H, W, f.device)
+    _lib.check(lib.gd_filter_power(f.data_ptr(), out.data_ptr(), N, H, W, ws.data_ptr(), _stream()),
+               "gd_filter_power")
+    return out
+
+
+def tikhonov(y, psf, alpha, lam, ltl=None):
+    """models/Tikhonet.py:15-31 (Tikhonov.forward) on the HIP engine: Re IFFT2(conj(H) FFT2(y/alpha) /
+    (|H|^2 + lam LtL)); ``ltl`` None = filter 'Identity', else a half-spectrum [1|N, W//2+1, H]."""
+    _require_device(y, psf, alpha, lam, ltl)
+    lib = _lib.load()
+    y = _img(y, "y")
+    N, _, H, W = y.shape
+    k, gs = _psf(psf, N, H)
+    al, al_s = _galaxy_scalar(alpha, N, "alpha")
+    lm, lm_s = _galaxy_scalar(lam.detach() if torch.is_tensor(lam) else lam, N, "lam")
+    lptr, lgs = None, 0
+    if ltl is not None:
+        K = W // 2 + 1
+        ltl = ltl.float().contiguous()
+        if ltl.shape[-2:] != (K, H) or ltl.numel() not in (K * H, N * K * H):
+            raise ValueError(f"ltl must be [1|N, {K}, {H}], got {tuple(ltl.shape)}")
+        lptr, lgs = ltl.data_ptr(), (0 if ltl.numel() == K * H else K * H)
+    out = torch.empty_like(y)
+    ws = workspace(N, H, W, y.device)
+    _lib.check(lib.gd_tikhonov(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
+                               lm.data_ptr(), lm_s, lptr, lgs, out.data_ptr(), N, H, W, ws.data_ptr(), _stream()),
+               "gd_tikhonov")
+    return out
+
+
 def subnet_features(otf128, params):
     """SubNet conv features [N, 1024] from the 128x128 half-spectrum OTF of the PSFs
     (``k_subnet_features``; ``params`` packed as documented in include/gdeconv.h)."""
@@ -243,4 +282,5 @@ class ADMMState:
 
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
+           "tikhonov", "filter_power",
            "ADMMState", "workspace", "empty_otf", "supported", "subnet_features"]

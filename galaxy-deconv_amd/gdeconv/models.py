@@ -7,6 +7,8 @@
   (``self.init``) stay in PyTorch; every spectral step goes through ``gdeconv.engine``.
 * ``Wiener().forward(y, psf, alpha)`` - ``models/Wiener.py:10-20``.
 * ``Richard_Lucy(n_iters).forward(y, psf)`` - ``models/Richard_Lucy.py:10-24``.
+* ``Tikhonov(filter).forward(y, psf, alpha, lam)`` / ``Tikhonet(filter)`` - ``models/Tikhonet.py:8-47``
+  (the Tikhonov solve on the engine, the XDenseUNet denoiser in PyTorch).
 
 Differences from the reference, all deliberate: the device is taken from the input (the reference
 hard-codes ``cuda:0``, ``models/Unrolled_ADMM.py:178``), the OTF is computed on the device (the
@@ -19,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import engine
-from .nets import SubNet, ZUpdateResUNet
+from .nets import SubNet, XDenseUNet, ZUpdateResUNet
 
 
 def _rho_view(rho_iters, n, N):
@@ -94,4 +96,67 @@ class Richard_Lucy(nn.Module):
         return engine.richardson_lucy(y, psf, self.n_iters)
 
 
-__all__ = ["Unrolled_ADMM", "Wiener", "Richard_Lucy"]
+def laplacian_kernel():
+    """utils/utils_torch.py:95-99: the 3x3 Laplacian stencil [1,1,3,3]."""
+    return torch.tensor([[[[0.0, 1.0, 0.0], [1.0, -4.0, 1.0], [0.0, 1.0, 0.0]]]])
+
+
+def placed_filter(ker, H, W, device):
+    """The image ``psf_to_otf(ker, [1,1,H,W])[0]`` builds (utils/utils_torch.py:79-92), INCLUDING its
+    behaviour for an odd 3x3 kernel: with ``center = 2`` the quadrant copies broadcast the 1-wide
+    slices ``ker[2:, 2:]``, ``ker[2:, :2]``, ``ker[:2, 2:]`` over 2x2 blocks, so the Laplacian the
+    reference regularises with is NOT the centred stencil.  Constant, built once per size (plumbing)."""
+    k = ker.reshape(ker.shape[-2], ker.shape[-1]).float()
+    img = torch.zeros(H, W)
+    c = (k.shape[0] + 1) // 2
+    img[:c, :c] = k[c:, c:]
+    img[:c, -c:] = k[c:, :c]
+    img[-c:, :c] = k[:c, c:]
+    img[-c:, -c:] = k[:c, :c]
+    return img.view(1, 1, H, W).to(device)
+
+
+class Tikhonov(nn.Module):
+    """models/Tikhonet.py:8-31: x = Re IFFT2(conj(H) FFT2(y/alpha) / (|H|^2 + lam [|L|^2])).  The
+    Laplacian's |L|^2 is computed on the device once per (size, device) and cached."""
+
+    def __init__(self, filter="Identity"):
+        super().__init__()
+        if filter not in ("Identity", "Laplacian"):
+            raise ValueError("filter must be 'Identity' or 'Laplacian'")
+        self.filter = filter
+        if self.filter == "Laplacian":
+            self.lap = laplacian_kernel()
+        self._ltl = {}
+
+    def ltl(self, H, W, device):
+        key = (H, W, str(device))
+        if key not in self._ltl:
+            self._ltl[key] = engine.filter_power(placed_filter(self.lap, H, W, device))
+        return self._ltl[key]
+
+    def forward(self, y, psf, alpha, lam):
+        ltl = self.ltl(y.shape[-2], y.shape[-1], y.device) if self.filter == "Laplacian" else None
+        if not torch.is_tensor(lam):
+            lam = torch.tensor(float(lam))
+        return engine.tikhonov(y, psf, alpha, lam.to(y.device), ltl)
+
+
+class Tikhonet(nn.Module):
+    """models/Tikhonet.py:34-47: max(y, 0) -> Tikhonov(lam) -> XDenseUNet -> times alpha.  ``lam`` is
+    a plain tensor as in the reference (not a Parameter, not in the state_dict)."""
+
+    def __init__(self, filter="Identity"):
+        super().__init__()
+        self.tikhonov = Tikhonov(filter=filter)
+        self.denoiser = XDenseUNet()
+        self.lam = torch.tensor(1.0, requires_grad=True)
+
+    def forward(self, y, psf, alpha):
+        y = torch.clamp_min(y, 0.0)
+        x = self.tikhonov(y, psf, alpha, self.lam)
+        x = self.denoiser(x)
+        return x * alpha
+
+
+__all__ = ["Unrolled_ADMM", "Wiener", "Richard_Lucy", "Tikhonov", "Tikhonet", "laplacian_kernel"]

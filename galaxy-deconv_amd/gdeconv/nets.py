@@ -210,3 +210,89 @@ def count_params(m):
 
 
 __all__ = ["ResUNet", "ResBlock", "ZUpdateResUNet", "SubNet", "count_params"]
+
+
+# ---------------------------------------------------------------------------- Tikhonet denoiser
+# XDenseUNet (``models/XDenseUNet.py``): a 3-level dense U-Net on 48x48 stamps, used by Tikhonet /
+# ShapeNet after the Tikhonov solve.  PyTorch-ROCm (host side, not the spectral path).  Module tree
+# laid out for the reference checkpoints' keys (``saved_models/Tikhonet_*_50epochs.pth``):
+#   <block>.net.<i>.{0: BatchNorm2d, 2: SepConv.depthewise / .pointwise}   dense layers
+#   Down: net.{0: BatchNorm2d, 2: Conv2d 1x1}   (then MaxPool2d(2))
+#   Up:   net.{0: Conv2d 1x1 with bias}         (then nearest x2 upsampling)
+class SepConv(nn.Module):
+    """Depthwise k x k ('same' padding) then pointwise 1x1, no bias (``XDenseUNet.py:5-16``).
+    The attribute name ``depthewise`` is the checkpoints' spelling."""
+
+    def __init__(self, cin, cout, k=3):
+        super().__init__()
+        self.depthewise = nn.Conv2d(cin, cin, k, padding="same", groups=cin, bias=False)
+        self.pointwise = nn.Conv2d(cin, cout, 1, bias=False)
+
+    def forward(self, x):
+        return self.pointwise(self.depthewise(x))
+
+
+class DenseBlock(nn.Module):
+    """``num_layers`` x [BN, ReLU, SepConv(c -> growth)], each output PREPENDED to the running stack
+    (``torch.cat((out, y))``); ``skip`` prepends the block input once more (``XDenseUNet.py:19-41``)."""
+
+    def __init__(self, num_layers, cin, growth=12, k=3, skip=False):
+        super().__init__()
+        self.skip_connection = skip
+        self.net = nn.Sequential(*[
+            nn.Sequential(nn.BatchNorm2d(cin + i * growth), nn.ReLU(inplace=True),
+                          SepConv(cin + i * growth, growth, k))
+            for i in range(num_layers)])
+
+    def forward(self, x):
+        y = x
+        for layer in self.net:
+            y = torch.cat((layer(y), y), dim=1)
+        return torch.cat((x, y), dim=1) if self.skip_connection else y
+
+
+class DenseDown(nn.Module):
+    """BN, ReLU, 1x1 conv (no bias), 2x2 max-pool (``XDenseUNet.py:44-55``)."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.net = nn.Sequential(nn.BatchNorm2d(cin), nn.ReLU(inplace=True),
+                                 nn.Conv2d(cin, cout, 1, bias=False), nn.MaxPool2d(2, 2))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class DenseUp(nn.Module):
+    """1x1 conv with bias, nearest x2 upsampling (``XDenseUNet.py:58-67``)."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.net = nn.Sequential(nn.Conv2d(cin, cout, 1, bias=True), nn.Upsample(scale_factor=(2, 2), mode="nearest"))
+
+    def forward(self, x):
+        return self.net(x)
+
+
+class XDenseUNet(nn.Module):
+    """``models/XDenseUNet.py:70-112``: channels 1 -> 112 (48^2) -> 220 (24^2) -> 352 (12^2) -> body
+    at 6^2 -> 84 -> 72 -> 60 -> 1, skips by concatenation."""
+
+    def __init__(self):
+        super().__init__()
+        self.input = nn.Sequential(nn.Conv2d(1, 32, 3, padding="same", bias=False), DenseBlock(4, 32, skip=True))
+        self.down1 = nn.Sequential(DenseDown(112, 80), DenseBlock(5, 80, skip=True))
+        self.down2 = nn.Sequential(DenseDown(220, 140), DenseBlock(6, 140, skip=True))
+        self.body = nn.Sequential(DenseDown(352, 212), DenseBlock(7, 212), DenseUp(296, 84))
+        self.up1 = nn.Sequential(DenseBlock(6, 436), DenseUp(508, 72))
+        self.up2 = nn.Sequential(DenseBlock(5, 292), DenseUp(352, 60))
+        self.output = nn.Sequential(DenseBlock(4, 172), nn.Conv2d(220, 1, 1, bias=True))
+
+    def forward(self, x):
+        x1 = self.input(x)
+        x2 = self.down1(x1)
+        x3 = self.down2(x2)
+        x4 = self.body(x3)
+        x5 = self.up1(torch.cat((x3, x4), dim=1))
+        x6 = self.up2(torch.cat((x2, x5), dim=1))
+        return self.output(torch.cat((x1, x6), dim=1))

@@ -22,6 +22,8 @@
  *                       :212-213, next V step, output scaling :215)
  *   gd_wiener           models/Wiener.py:10-20       Wiener.forward(y, psf, alpha)
  *   gd_richardson_lucy  models/Richard_Lucy.py:10-24 Richard_Lucy(n_iters).forward(y, psf)
+ *   gd_tikhonov         models/Tikhonet.py:15-31     Tikhonov(filter).forward(y, psf, alpha, lam)
+ *   gd_filter_power     models/Tikhonet.py:26-27     LtL = |psf_to_otf(laplacian_kernel(), y.size())|^2
  */
 #ifndef GDECONV_H
 #define GDECONV_H
@@ -32,7 +34,7 @@
 extern "C" {
 #endif
 
-#define GD_ABI_VERSION 2
+#define GD_ABI_VERSION 3
 
 #define GD_OK 0
 #define GD_ERR_ARG (-1)
@@ -93,6 +95,18 @@ int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, in
 /* Richardson-Lucy from x0 = max(y,0); otf_half receives the OTF (gd_otf_bytes). */
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
+
+/* Tikhonov solve: x = Re IFFT2(conj(H) FFT2(y/alpha) / (|H|^2 + lam * LtL)); ltl = NULL is the
+ * 'Identity' filter (divisor |H|^2 + lam).  ltl: real half spectra [*][W/2+1][H] (transposed, as the
+ * OTF), ltl_gstride elements between galaxies (0 = one shared filter), e.g. from gd_filter_power.
+ * lam: per-galaxy scalar (stride 0 = the reference's single learnable lambda). */
+int gd_tikhonov(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+                long long alpha_stride, const float* lam, long long lam_stride, const float* ltl,
+                long long ltl_gstride, float* x, int N, int H, int W, void* ws, void* stream);
+
+/* power_half[g][kx][ky] = |FFT2(filt[g])|^2 over the half spectrum (filt: real images [N][H][W],
+ * any placement, e.g. the circularly shifted Laplacian of the reference's psf_to_otf). */
+int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, void* ws, void* stream);
 
 /* SubNet feature extractor (models/Unrolled_ADMM.py:77-84): from the 128x128 half-spectrum OTF
  * of the PSFs (gd_psf_to_otf with H = W = 128; |OTF|^2 = |FFT2(pad128(psf))|^2), MaxPool2 and the

@@ -21,6 +21,7 @@ Reference call sites followed (paths relative to the reference root):
   admm_forward        models/Unrolled_ADMM.py:177-215
   wiener              models/Wiener.py:10-20
   richardson_lucy     models/Richard_Lucy.py:10-24
+  tikhonov            models/Tikhonet.py:15-31 (+ laplacian_kernel, utils/utils_torch.py:95-99)
 """
 import torch
 
@@ -138,6 +139,25 @@ def richardson_lucy(y, psf, n_iters):
     return x
 
 
+def laplacian_kernel():
+    """utils/utils_torch.py:95-99."""
+    return torch.tensor([[[[0.0, 1.0, 0.0], [1.0, -4.0, 1.0], [0.0, 1.0, 0.0]]]])
+
+
+def tikhonov(y, psf, alpha, lam, filt="Identity"):
+    """models/Tikhonet.py:15-31 (Tikhonov.forward; y taken as given - Tikhonet applies max(y,0)).
+    The Laplacian goes through psf_to_otf exactly as the reference's (odd 3x3: broadcast quadrants)."""
+    _, H = psf_to_otf(psf, y.size(), dtype=y.dtype)
+    Ht, HtH = torch.conj(H), torch.abs(H) ** 2
+    numerator = Ht * torch.fft.fftn(y / alpha, dim=[2, 3])
+    if filt == "Identity":
+        divisor = HtH + lam
+    else:
+        _, Lf = psf_to_otf(laplacian_kernel().to(y.dtype), y.size(), dtype=y.dtype)
+        divisor = HtH + lam * torch.abs(Lf) ** 2
+    return torch.real(torch.fft.ifftn(numerator / divisor, dim=[2, 3]))
+
+
 def normwise_error(out, ref):
     """Per-galaxy max|out - ref| / max|ref| (the parity metric of SURVEY.md 8(d)); returns [N]."""
     out = out.detach().double().cpu().reshape(out.shape[0], -1)
@@ -146,4 +166,5 @@ def normwise_error(out, ref):
 
 
 __all__ = ["psf_to_otf", "conv_fft_batch", "x_update", "v_update_poisson", "v_update_gaussian",
-           "init_l2", "admm_forward", "wiener", "richardson_lucy", "normwise_error"]
+           "init_l2", "admm_forward", "wiener", "richardson_lucy", "tikhonov", "laplacian_kernel",
+           "normwise_error"]

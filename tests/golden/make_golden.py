@@ -34,6 +34,11 @@ sys.path.insert(0, REF)
 
 from gdeconv.synth import make_batch           # noqa: E402
 from gdeconv.weights import make_state_dict    # noqa: E402
+
+# the drop-in's regular package ``models`` would shadow the reference's namespace package
+sys.path[:] = [p for p in sys.path if os.path.abspath(p) != os.path.join(REPO, "galaxy-deconv_amd")]
+for _m in [m for m in sys.modules if m == "models" or m.startswith("models.")]:
+    del sys.modules[_m]
 from models.Unrolled_ADMM import Unrolled_ADMM  # noqa: E402  (reference)
 from models.Wiener import Wiener               # noqa: E402  (reference)
 from models.Richard_Lucy import Richard_Lucy   # noqa: E402  (reference)

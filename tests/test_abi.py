@@ -49,7 +49,8 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_host_only_queries(lib):
-    assert lib.gd_abi_version() == 2
+    from gdeconv import _lib as _lib_mod
+    assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 3
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
     assert lib.gd_supported_size(50, 50) == 0 and lib.gd_supported_size(256, 128) == 0
     # workspace: N * 2 images * (W/2+1) * H complex64

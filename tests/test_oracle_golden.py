@@ -96,3 +96,38 @@ def test_fp64_restatement_close_to_fp32_reference():
     obs, psf, alpha = T(g["obs"]).double(), T(g["psf"]).double(), T(g["alpha"]).double()
     out = O.admm_forward(obs, psf, alpha, T(g["Gaussian_rho1"]).double(), T(g["Gaussian_rho2"]).double())
     assert float(O.normwise_error(T(g["Gaussian_out"]), out).max()) < 2e-6
+
+
+@pytest.mark.parametrize("tag", ["48", "256"])
+@pytest.mark.parametrize("filt", ["Identity", "Laplacian"])
+def test_tikhonov(tag, filt):
+    """models/Tikhonet.py:15-31, including psf_to_otf's broadcast placement of the 3x3 Laplacian."""
+    g = golden("tikhonov.npz")
+    obs, psf, alpha = T(g[f"obs{tag}"]), T(g[f"psf{tag}"]), T(g[f"alpha{tag}"])
+    yp = torch.max(obs, torch.zeros_like(obs))
+    for lam in (1.0, 0.37):
+        out = O.tikhonov(yp, psf, alpha, torch.tensor(lam), filt)
+        assert torch.equal(out, T(g[f"tik_{filt}_{lam}_{tag}"]))
+
+
+@pytest.mark.parametrize("filt", ["Identity", "Laplacian"])
+def test_tikhonet_full_model(filt):
+    """Oracle Tikhonov + the host-side XDenseUNet mirror reproduce the reference Tikhonet."""
+    from gdeconv.nets import XDenseUNet
+    from gdeconv.weights import make_state_dict
+
+    class M(torch.nn.Module):  # the reference Tikhonet's module tree: tikhonov (no params) + denoiser
+        def __init__(self):
+            super().__init__()
+            self.denoiser = XDenseUNet()
+
+    torch.set_num_threads(8)
+    g = golden("tikhonov.npz")
+    obs, psf, alpha = T(g["obs48"]), T(g["psf48"]), T(g["alpha48"])
+    m = M()
+    m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    m.eval()
+    with torch.no_grad():
+        x = O.tikhonov(torch.max(obs, torch.zeros_like(obs)), psf, alpha, torch.tensor(1.0), filt)
+        out = m.denoiser(x) * alpha
+    assert torch.equal(out, T(g[f"tikhonet_{filt}_48"]))
