@@ -79,11 +79,12 @@ struct Args {
     long long ltl_gstride; // elements between galaxies' |L|^2 (0 = one shared filter)
 };
 
-enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR };
+enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
+                  RF_PADV, RF_PSF_YPAD, RF_PAD2 };  // RF_PAD*: L/2 x L/2 sources zero-padded to L x L
 enum ColMode { C_ITER, C_OTF_INIT, C_OTF_CONV, C_WIENER, C_OTF, C_CONV, C_CONVC, C_CONV2, C_FWD, C_INV,
                C_G_INIT, C_G_ITER, C_G_W1, C_G_ITER_F, C_G_ITER_L, C_G_ITER_FL,  // _F first, _L last iteration
-               C_TIKHONOV, C_POWER };
-enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL };
+               C_TIKHONOV, C_POWER, C_GX_INIT, C_GX, C_GX_BWD };
+enum RowInvMode { RI_ITER, RI_INIT, RI_OUT1, RI_OUT2, RI_RL_FINAL, RI_CROP, RI_CROP_BWD };  // RI_CROP*: L/2 x L/2 sinks
 enum RowInvFwdMode { RIF_CLAMP, RIF_RL_RATIO, RIF_RL_UPDATE };
 
 constexpr int rows_per_block(int lpb, int L) {
@@ -189,7 +190,7 @@ __device__ __forceinline__ void gather_rows(const Args& a, float2* rowbuf, int g
 // ---------------------------------------------------------------- RF: row forward
 template <int MODE>
 struct RfTraits {
-    static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE || MODE == RF_YA) ? 1 : 2;
+    static constexpr int NI = (MODE == RF_PSF || MODE == RF_ONE || MODE == RF_YA || MODE == RF_PADV) ? 1 : 2;
 };
 
 // Four consecutive pixels of image `im` starting at flat pixel index `pix` (row-major, 16-byte
@@ -227,6 +228,39 @@ __device__ __forceinline__ float4 rf_source4(const Args& a, int g, int im, int r
         } else {
             const float al = a.alpha(g);                               // max(y,0) / alpha
             return make_float4(yp.x / al, yp.y / al, yp.z / al, yp.w / al);
+        }
+    } else if constexpr (MODE == RF_PADV || MODE == RF_PSF_YPAD || MODE == RF_PAD2) {
+        // UnrolledADMMGaussian (models/unrolled_admm_gaussian.py): sources are Lh x Lh images placed at
+        // the origin of the 2Lh x 2Lh grid.  pad_double + ifftshift put pixel i at (i - Lh/2) mod 2Lh
+        // instead; that shift is a common phase of every spectrum, which cancels in conj(H) Y and |H|^2
+        // and is undone by fftshift + crop_half.
+        constexpr int Lh = L / 2;
+        if constexpr (MODE == RF_PSF_YPAD) {
+            if (im == 0)                                               // PSF (Lh x Lh) centred on (0,0)
+                return make_float4(shifted_psf(a, g, r, c, L), shifted_psf(a, g, r, c + 1, L),
+                                   shifted_psf(a, g, r, c + 2, L), shifted_psf(a, g, r, c + 3, L));
+        }
+        if (r >= Lh || c >= Lh) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const size_t p = ((size_t)g * Lh + r) * Lh + c;
+        if constexpr (MODE == RF_PSF_YPAD) {                           // max(y, 0)
+            const float4 y = ld4(a.y + p);
+            return make_float4(fmaxf(y.x, 0.f), fmaxf(y.y, 0.f), fmaxf(y.z, 0.f), fmaxf(y.w, 0.f));
+        } else if constexpr (MODE == RF_PAD2) {
+            return ld4((im == 0 ? a.a0 : a.a1) + p);
+        } else {
+            // rho z - u (XUpdateGaussian :91), optionally after the dual update of the previous
+            // iteration u = u + rho_prev (x_prev - z) (:145), written back in place (o1 = a1)
+            const float4 z = ld4(a.a0 + p);
+            const float rho = a.rho1(g);
+            float4 u = a.a1 ? ld4(a.a1 + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.a2) {
+                const float4 xp = ld4(a.a2 + p);
+                const float rp = a.rho2(g);
+                u = make_float4(u.x + rp * (xp.x - z.x), u.y + rp * (xp.y - z.y), u.z + rp * (xp.z - z.z),
+                                u.w + rp * (xp.w - z.w));
+                st4(a.o1 + p, u);
+            }
+            return make_float4(rho * z.x - u.x, rho * z.y - u.y, rho * z.z - u.z, rho * z.w - u.w);
         }
     } else if constexpr (MODE == RF_ONE) {
         return ld4(a.a0 + pix);
@@ -282,7 +316,8 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI, RBX>::THREADS)) void
 template <int MODE>
 struct ColTraits {
     static constexpr bool IN2 = (MODE == C_ITER || MODE == C_OTF_INIT || MODE == C_OTF_CONV ||
-                                 MODE == C_WIENER || MODE == C_CONV2 || MODE == C_TIKHONOV);
+                                 MODE == C_WIENER || MODE == C_CONV2 || MODE == C_TIKHONOV || MODE == C_GX_INIT ||
+                                 MODE == C_GX_BWD);
     static constexpr bool OUT2 = (MODE == C_ITER || MODE == C_CONV2);
     static constexpr bool HAS_OUT = (MODE != C_OTF && MODE != C_FWD && MODE != C_G_W1 && MODE != C_POWER);
     static constexpr bool STORE_OTF = (MODE == C_OTF_INIT || MODE == C_OTF_CONV || MODE == C_OTF);
@@ -417,7 +452,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
-    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_INIT) ? a.alpha(g) : 1.f;
+    const float al = (MODE == C_OTF_INIT || MODE == C_WIENER || MODE == C_G_INIT || MODE == C_GX_INIT) ? a.alpha(g) : 1.f;
+    const float rgx = (MODE == C_GX || MODE == C_GX_BWD) ? a.rho1(g) : 0.f;
+    float drho = 0.f;  // C_GX_BWD: this lane's part of d loss / d rho
     const float lam = (MODE == C_TIKHONOV) ? a.rho1(g) : 0.f;  // Tikhonov lambda rides in rho1
     constexpr bool giter = (MODE == C_G_ITER || MODE == C_G_ITER_F || MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
     constexpr bool gfirst = (MODE == C_G_ITER_F || MODE == C_G_ITER_FL);
@@ -430,7 +467,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         const int ky = j + F1 * s;
         float2 Hk = make_float2(0.f, 0.f);
         if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
-        if constexpr (TR::STORE_OTF || MODE == C_WIENER) Hk = P[s];
+        if constexpr (TR::STORE_OTF || MODE == C_WIENER || MODE == C_TIKHONOV) Hk = P[s];
         if constexpr (TR::STORE_OTF) {
             if (valid) a.otf[ob + ky] = Hk;
         }
@@ -485,6 +522,38 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float div = a.ltl ? HtH + lam * a.ltl[(size_t)g * a.ltl_gstride + (size_t)kx * L + ky] : HtH + lam;
             const float2 num = cmulc(Q[s], Hk);
             P[s] = cscale(make_float2(num.x / div, num.y / div), inv_n);
+        } else if constexpr (MODE == C_GX_INIT) {
+            // UnrolledADMMGaussian (models/unrolled_admm_gaussian.py:111-127): H from the PSF, Y = F(max(y,0));
+            // state |H|^2 and G = Y conj(H); x0 spectrum (Y Ht) / (HtH + 1/alpha)
+            const float2 Hk2 = P[s];
+            const float hh = Hk2.x * Hk2.x + Hk2.y * Hk2.y;
+            const float2 Gk = cmulc(Q[s], Hk2);
+            if (valid) {
+                a.s_hh[ob + ky] = hh;
+                a.s_g[ob + ky] = Gk;
+            }
+            const float lhs = hh + 1.0f / al;
+            P[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+        } else if constexpr (MODE == C_GX) {
+            // XUpdateGaussian (:89-93): X = (Ht Y + F(rho z - u)) / (rho + HtH); X kept for the backward
+            const float hh = a.s_hh[ob + ky];
+            const float2 Gk = a.s_g[ob + ky];
+            const float lhs = rgx + hh;
+            const float2 rhs = cadd(Gk, P[s]);
+            const float2 X = make_float2(rhs.x / lhs, rhs.y / lhs);
+            if (a.s_w && valid) a.s_w[ob + ky] = X;
+            P[s] = cscale(X, inv_n);
+        } else if constexpr (MODE == C_GX_BWD) {
+            // adjoint of the X update (self-adjoint: real, symmetric 1/D): dv = crop IFFT(F(pad g) / D);
+            // d/drho = <pad g, IFFT((F(pad z) - X) / D)> = (1/L^2) sum_k Re(conj(Gg) (Z - X)) / D over the
+            // full spectrum: half-spectrum bins other than kx = 0, L/2 count twice
+            const float hh = a.s_hh[ob + ky];
+            const float D = rgx + hh;
+            const float2 X = a.s_w[ob + ky];
+            const float2 d = csub(Q[s], X);
+            const float wk = (kx == 0 || 2 * kx == L) ? 1.f : 2.f;
+            drho += wk * (P[s].x * d.x + P[s].y * d.y) / D;
+            P[s] = cscale(make_float2(P[s].x / D, P[s].y / D), inv_n);
         } else if constexpr (MODE == C_POWER) {
             // |F(x)|^2 of a real filter image (the Laplacian's LtL, models/Tikhonet.py:26-27)
             if (valid) a.s_hh[ob + ky] = P[s].x * P[s].x + P[s].y * P[s].y;
@@ -500,6 +569,11 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         } else if constexpr (MODE == C_INV) {
             P[s] = cscale(P[s], inv_n);
         }
+    }
+    if constexpr (MODE == C_GX_BWD) {
+#pragma unroll
+        for (int off = F1 / 2; off > 0; off >>= 1) drho += __shfl_xor(drho, off, F1);
+        if (valid && j == 0) a.o2[(size_t)g * K + kx] = drho * inv_n;
     }
     if constexpr (TR::HAS_OUT && MODE != C_FWD && VAR != 1) {
         line_fft<L, true>(P, j, my, tw);
@@ -853,6 +927,28 @@ __global__ __launch_bounds__((RowGeo<L, RiTraits<MODE>::NI, RBX>::THREADS)) void
         if (!(MODE == RI_ITER && a.last)) r2n = a.rho2n(g);
     }
     if constexpr (MODE == RI_RL_FINAL) div = a.otf[(size_t)g * G::K * L].x;  // conv(Ht, ones) = H(0,0)
+    if constexpr (MODE == RI_CROP || MODE == RI_CROP_BWD) {
+        // UnrolledADMMGaussian: crop_half(fftshift(.)) = the Lh x Lh corner at the origin (see RF_PADV)
+        constexpr int Lh = L / 2;
+        const float rho = (MODE == RI_CROP_BWD || a.o2) ? a.rho1(g) : 0.f;
+        for (int q = tid * 4; q < R::RB * L; q += R::THREADS * 4) {
+            const int rr = q / L, c = q - rr * L, r = row0 + rr;
+            if (r >= Lh || c >= Lh) continue;
+            const size_t p = ((size_t)g * Lh + r) * Lh + c;
+            const float4 X = ld4(res + rr * L + c);
+            if constexpr (MODE == RI_CROP) {
+                st4(a.o0 + p, X);                                  // x (or z0 = init_l2)
+                if (a.o2) {                                        // next denoiser input rho x + u (:142)
+                    const float4 u = a.a1 ? ld4(a.a1 + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    st4(a.o2 + p, make_float4(rho * X.x + u.x, rho * X.y + u.y, rho * X.z + u.z, rho * X.w + u.w));
+                }
+            } else {                                               // dz = rho dv, du = -dv
+                st4(a.o0 + p, make_float4(rho * X.x, rho * X.y, rho * X.z, rho * X.w));
+                st4(a.o1 + p, make_float4(-X.x, -X.y, -X.z, -X.w));
+            }
+        }
+        return;
+    }
     const bool poisson = a.llh == GD_LLH_POISSON;
     // elementwise sink over this block's RB x L pixels, 4 consecutive pixels per thread step
     for (int q = tid * 4; q < R::RB * L; q += R::THREADS * 4) {
@@ -1268,6 +1364,22 @@ struct Ops {
             return Lc::template ri<RI_OUT1>(a, st);
         });
     }
+    // UnrolledADMMGaussian on the 2x-padded grid (this L = 2 x image side); one pass over the batch
+    static int gx_init(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_PSF_YPAD>(a, st));
+        GD_TRY(Lc::template col<C_GX_INIT>(a, st));
+        return Lc::template ri<RI_CROP>(a, st);
+    }
+    static int gx_x(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_PADV>(a, st));
+        GD_TRY(Lc::template col<C_GX>(a, st));
+        return Lc::template ri<RI_CROP>(a, st);
+    }
+    static int gx_x_bwd(Args a, hipStream_t st) {
+        GD_TRY(Lc::template rf<RF_PAD2>(a, st));
+        GD_TRY(Lc::template col<C_GX_BWD>(a, st));
+        return Lc::template ri<RI_CROP_BWD>(a, st);
+    }
     static int power(Args a, hipStream_t st) {
         GD_TRY(Lc::template rf<RF_ONE>(a, st));
         return Lc::template col<C_POWER>(a, st);
@@ -1527,6 +1639,74 @@ int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, v
     a.a0 = filt;
     a.s_hh = power_half;
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::power(a, (hipStream_t)stream); });
+}
+
+namespace {
+int check_gx(int N, int H, int W) {
+    if (N < 0) return fail(GD_ERR_ARG, "negative batch");
+    if (H != W || !gd_supported_size(2 * H, 2 * W) || H % 4)
+        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: square images of side 32, 48, 64 or 128 (2x padded grid)");
+    return GD_OK;
+}
+void bind_gx_state(Args& a, void* state, int N, int H) {
+    const size_t spec = (size_t)N * (H + 1) * (2 * H);  // half spectrum of the 2H x 2H grid
+    a.s_hh = reinterpret_cast<float*>(state);
+    a.s_g = reinterpret_cast<float2*>(state) + spec / 2;
+}
+}  // namespace
+
+size_t gd_gx_state_bytes(int N, int H, int W) {
+    if (check_gx(N, H, W) != GD_OK || N <= 0) return 0;
+    return (size_t)N * (H + 1) * (2 * H) * (sizeof(float) + sizeof(float2));
+}
+
+size_t gd_gx_spec_bytes(int N, int H, int W) {
+    if (check_gx(N, H, W) != GD_OK || N <= 0) return 0;
+    return (size_t)N * (H + 1) * (2 * H) * sizeof(float2);
+}
+
+int gd_gx_init(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+               long long alpha_stride, int N, int H, int W, void* state, float* z0, void* ws, void* stream) {
+    GD_TRY(check_gx(N, H, W));
+    if (h != H || w != W) return fail(GD_ERR_ARG, "UnrolledADMMGaussian pads the PSF like the image: psf must be H x W");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, 2 * H);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    bind_gx_state(a, state, N, H);
+    a.o0 = z0;
+    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_init(a, (hipStream_t)stream); });
+}
+
+int gd_gx_xupdate(const float* z, float* u, const float* x_prev, const float* rho, long long rho_stride,
+                  const float* rho_prev, long long rho_prev_stride, float* x, float* zin, void* xspec,
+                  int N, int H, int W, void* state, void* ws, void* stream) {
+    GD_TRY(check_gx(N, H, W));
+    if (x_prev && (!u || !rho_prev)) return fail(GD_ERR_ARG, "the fused dual update needs u and rho_prev");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, 2 * H);
+    bind_gx_state(a, state, N, H);
+    a.a0 = z; a.a1 = u; a.a2 = x_prev; a.o1 = u;
+    a.rho1 = GalScalar{rho, rho_stride};
+    a.rho2 = GalScalar{rho_prev ? rho_prev : rho, rho_prev ? rho_prev_stride : rho_stride};
+    a.s_w = reinterpret_cast<float2*>(xspec);
+    a.o0 = x; a.o2 = zin;
+    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_x(a, (hipStream_t)stream); });
+}
+
+int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho, long long rho_stride,
+                           const void* xspec, float* grad_z, float* grad_u, float* grad_rho_part, int N, int H,
+                           int W, void* state, void* ws, void* stream) {
+    GD_TRY(check_gx(N, H, W));
+    if (!xspec) return fail(GD_ERR_ARG, "backward needs the forward's saved spectrum");
+    if (N == 0) return GD_OK;
+    Args a = base_args(N, ws, 2 * H);
+    bind_gx_state(a, state, N, H);
+    a.a0 = grad_x; a.a1 = z;
+    a.rho1 = GalScalar{rho, rho_stride};
+    a.s_w = reinterpret_cast<float2*>(const_cast<void*>(xspec));
+    a.o0 = grad_z; a.o1 = grad_u; a.o2 = grad_rho_part;
+    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_x_bwd(a, (hipStream_t)stream); });
 }
 
 int gd_profile_enable(int level) {

@@ -41,6 +41,11 @@ SIGNATURES = {
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
     "gd_tikhonov": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_filter_power": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "gd_gx_state_bytes": (_SZ, [_I, _I, _I]),
+    "gd_gx_spec_bytes": (_SZ, [_I, _I, _I]),
+    "gd_gx_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _I, _I, _I, _P, _P, _P, _P]),
+    "gd_gx_xupdate": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "gd_gx_xupdate_backward": (_I, [_P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "gd_set_chunk_bytes": (_SZ, [_SZ]),
     "gd_set_pipeline_streams": (_I, [_I]),
     "gd_set_fused_iteration": (_I, [_I]),

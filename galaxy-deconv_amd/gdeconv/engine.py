@@ -215,6 +215,111 @@ def subnet_features(otf128, params):
     return feat
 
 
+class GaussXState:
+    """Device state of one ``UnrolledADMMGaussian`` forward (models/unrolled_admm_gaussian.py:117-152):
+    |H|^2 and G = F(max(y,0)) conj(H) on the 2x zero-padded grid (gd_gx_init), a private workspace.
+    Images and PSFs are H x W (the PSF is padded like the image, so it must have the image's size)."""
+
+    def __init__(self, y, psf, alpha):
+        _require_device(y, psf, alpha)
+        self.lib = _lib.load()
+        self.y = _img(y, "y")
+        self.N, _, self.H, self.W = self.y.shape
+        self.psf, self.psf_gs = _psf(psf, self.N, self.H)
+        if tuple(self.psf.shape[-2:]) != (self.H, self.W):
+            raise ValueError("UnrolledADMMGaussian pads the PSF like the image: psf must be H x W "
+                             "(pad_double(kernel) at models/unrolled_admm_gaussian.py:122)")
+        self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha")
+        N1 = max(self.N, 1)
+        nbytes = int(self.lib.gd_gx_state_bytes(N1, self.H, self.W))
+        if nbytes == 0:
+            raise ValueError(f"UnrolledADMMGaussian: unsupported image size {self.H}x{self.W} "
+                             "(supported: square 32, 48, 64, 128)")
+        dev = self.y.device
+        self.state = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.ws = torch.empty(int(self.lib.gd_workspace_bytes(N1, 2 * self.H, 2 * self.W)), dtype=torch.uint8,
+                              device=dev)
+        self.spec_bytes = int(self.lib.gd_gx_spec_bytes(N1, self.H, self.W))
+
+    def init(self):
+        """z0 = init_l2(Y, Ht, HtH, alpha) (:111-115)."""
+        z0 = torch.empty_like(self.y)
+        k = self.psf
+        _lib.check(self.lib.gd_gx_init(self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3],
+                                       self.alpha.data_ptr(), self.alpha_s, self.N, self.H, self.W,
+                                       self.state.data_ptr(), z0.data_ptr(), self.ws.data_ptr(), _stream()),
+                   "gd_gx_init")
+        return z0
+
+    def rho(self, rho):
+        return _galaxy_scalar(rho.detach() if torch.is_tensor(rho) else rho, self.N, "rho")
+
+    def x_update(self, z, u, rho, x_prev=None, rho_prev=None, zin=False, save=False):
+        """x = XUpdateGaussian(Y, Ht, HtH, z, u, rho) (:85-93).  ``u`` None = 0.  ``x_prev`` given:
+        u <- u + rho_prev (x_prev - z) in place first (the dual update :145 of the previous
+        iteration).  Returns (x, rho x + u if zin, saved X spectrum if save)."""
+        z = _img(z, "z")
+        r, rs = self.rho(rho)
+        if x_prev is not None:
+            if u is None or rho_prev is None:
+                raise ValueError("the fused dual update needs u and rho_prev")
+            if not u.is_contiguous() or u.dtype != torch.float32:
+                raise ValueError("u is updated in place: it must be contiguous fp32")
+            x_prev = _img(x_prev, "x_prev")
+        elif u is not None:
+            u = _img(u, "u")
+        rp, rps = self.rho(rho_prev) if rho_prev is not None else (None, 0)
+        x = torch.empty_like(self.y)
+        zi = torch.empty_like(self.y) if zin else None
+        xs = torch.empty(self.spec_bytes, dtype=torch.uint8, device=self.y.device) if save else None
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        _lib.check(self.lib.gd_gx_xupdate(z.data_ptr(), ptr(u), ptr(x_prev), r.data_ptr(), rs, ptr(rp), rps,
+                                          x.data_ptr(), ptr(zi), ptr(xs), self.N, self.H, self.W,
+                                          self.state.data_ptr(), self.ws.data_ptr(), _stream()), "gd_gx_xupdate")
+        return x, zi, xs
+
+    def x_backward(self, grad_x, z, rho, xs):
+        """(dL/dz, dL/du, dL/drho [N]) of the X update from dL/dx (self-adjoint linear part)."""
+        g = _img(grad_x, "grad_x")
+        z = _img(z, "z")
+        r, rs = self.rho(rho)
+        gz, gu = torch.empty_like(self.y), torch.empty_like(self.y)
+        part = torch.empty(self.N, self.W + 1, dtype=torch.float32, device=self.y.device)
+        _lib.check(self.lib.gd_gx_xupdate_backward(g.data_ptr(), z.data_ptr(), r.data_ptr(), rs, xs.data_ptr(),
+                                                   gz.data_ptr(), gu.data_ptr(), part.data_ptr(), self.N, self.H,
+                                                   self.W, self.state.data_ptr(), self.ws.data_ptr(), _stream()),
+                   "gd_gx_xupdate_backward")
+        return gz, gu, part.sum(1)
+
+
+class _XUpdateGaussianFn(torch.autograd.Function):
+    """Autograd of XUpdateGaussian on the engine: x = M (rho z - u) + b(rho) with M self-adjoint, so
+    dz = rho M g, du = -M g, drho = <g, C IFFT((F(pad z) - X) / (rho + HtH))> (gd_gx_xupdate_backward)."""
+
+    @staticmethod
+    def forward(ctx, z, u, rho, st):
+        x, _, xs = st.x_update(z.detach(), u.detach(), rho, save=True)
+        ctx.st, ctx.xs = st, xs
+        ctx.rho_shape = rho.shape if torch.is_tensor(rho) else None
+        ctx.save_for_backward(z.detach().float().contiguous(), rho if torch.is_tensor(rho) else torch.tensor(rho))
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        z, rho = ctx.saved_tensors
+        st = ctx.st
+        gz, gu, grho = st.x_backward(gx.contiguous(), z, rho, ctx.xs)
+        gr = None
+        if ctx.needs_input_grad[2]:
+            gr = (grho.sum() if rho.numel() == 1 else grho).reshape(ctx.rho_shape).to(rho.dtype)
+        return (gz if ctx.needs_input_grad[0] else None, gu if ctx.needs_input_grad[1] else None, gr, None)
+
+
+def gx_x_update(st, z, u, rho):
+    """Differentiable X update of UnrolledADMMGaussian (autograd through the HIP backward)."""
+    return _XUpdateGaussianFn.apply(z, u, rho, st)
+
+
 class ADMMState:
     """Device state of one unrolled-ADMM forward: the engine's opaque state buffer (OTF + u1 and
     v - u2, spectral for llh='Gaussian', spatial for 'Poisson') and ``zin``, the next denoiser
@@ -282,5 +387,5 @@ class ADMMState:
 
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
-           "tikhonov", "filter_power",
+           "tikhonov", "filter_power", "GaussXState", "gx_x_update",
            "ADMMState", "workspace", "empty_otf", "supported", "subnet_features"]

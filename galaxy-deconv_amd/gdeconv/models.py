@@ -7,6 +7,9 @@
   (``self.init``) stay in PyTorch; every spectral step goes through ``gdeconv.engine``.
 * ``Wiener().forward(y, psf, alpha)`` - ``models/Wiener.py:10-20``.
 * ``Richard_Lucy(n_iters).forward(y, psf)`` - ``models/Richard_Lucy.py:10-24``.
+* ``UnrolledADMMGaussian(n_iters=8, denoiser='ResUNet', PnP=True, subnet=True, analysis=False)`` -
+  ``models/unrolled_admm_gaussian.py:96-152`` (the variant ``train.py:41`` trains): spectral steps
+  on the engine with a HIP backward for training; ResUNet(nc=32..256) and its SubNet in PyTorch.
 * ``Tikhonov(filter).forward(y, psf, alpha, lam)`` / ``Tikhonet(filter)`` - ``models/Tikhonet.py:8-47``
   (the Tikhonov solve on the engine, the XDenseUNet denoiser in PyTorch).
 
@@ -96,6 +99,62 @@ class Richard_Lucy(nn.Module):
         return engine.richardson_lucy(y, psf, self.n_iters)
 
 
+class XUpdateGaussian(nn.Module):
+    """models/unrolled_admm_gaussian.py:85-93 on the engine; the spectral constants (Y Ht, HtH) live
+    in the forward's ``GaussXState`` instead of being passed as full spectra."""
+
+    def forward(self, st, z, u, rho):
+        return engine.gx_x_update(st, z, u, rho)
+
+
+class UnrolledADMMGaussian(nn.Module):
+    """models/unrolled_admm_gaussian.py:96-152.  Same constructor, attributes and state_dict keys
+    (``Z.net.*`` with ResUNet nc=[32, 64, 128, 256], ``init.*`` SubNet with n outputs, or
+    ``rho_iters``).  Under ``torch.no_grad`` the X update, the previous iteration's dual update and the
+    next denoiser input ``rho x + u`` run fused in one engine call; with autograd on, the X update is
+    a custom Function with the engine's backward and the elementwise updates are PyTorch ops."""
+
+    def __init__(self, n_iters=8, denoiser="ResUNet", PnP=True, subnet=True, analysis=False):
+        super().__init__()
+        self.n_iters = n_iters
+        self.denoiser = denoiser
+        self.PnP = PnP
+        self.subnet = subnet
+        self.analysis = analysis
+        self.X = XUpdateGaussian()
+        self.Z = ZUpdateResUNet(nc=(32, 64, 128, 256))
+        if self.subnet:
+            self.init = SubNet(self.n_iters, n_out=self.n_iters, shift=True)
+        else:
+            self.rho_iters = nn.Parameter(torch.ones(size=[self.n_iters]), requires_grad=True)
+
+    def forward(self, y, kernel, alpha):
+        st = engine.GaussXState(y, kernel, alpha)       # max(y, 0) is applied on the device
+        rho_iters = self.init(kernel, alpha) if self.subnet else None
+        z = st.init()
+        u = torch.zeros_like(st.y)
+        x_list, z_list, u_list, rho_list = [], [], [], []
+        fused = not torch.is_grad_enabled() and not self.analysis
+        x, rho_prev = None, None
+        for i in range(self.n_iters):
+            rho = rho_iters[:, :, :, i].view(-1, 1, 1, 1) if self.subnet else self.rho_iters[i]
+            if fused:
+                x, zin, _ = st.x_update(z, u, rho, x_prev=x, rho_prev=rho_prev, zin=True)
+                z = self.Z(zin)
+                rho_prev = rho
+            else:
+                x = self.X(st, z, u, rho)
+                z = self.Z(rho * x + u)
+                u = u + rho * (x - z)
+                x_list.append(x)
+                z_list.append(z)
+                u_list.append(u)
+                rho_list.append(rho)
+        if self.analysis:
+            return x_list, z_list, u_list, rho_list
+        return z
+
+
 def laplacian_kernel():
     """utils/utils_torch.py:95-99: the 3x3 Laplacian stencil [1,1,3,3]."""
     return torch.tensor([[[[0.0, 1.0, 0.0], [1.0, -4.0, 1.0], [0.0, 1.0, 0.0]]]])
@@ -159,4 +218,5 @@ class Tikhonet(nn.Module):
         return x * alpha
 
 
-__all__ = ["Unrolled_ADMM", "Wiener", "Richard_Lucy", "Tikhonov", "Tikhonet", "laplacian_kernel"]
+__all__ = ["Unrolled_ADMM", "UnrolledADMMGaussian", "XUpdateGaussian", "Wiener", "Richard_Lucy", "Tikhonov",
+           "Tikhonet", "laplacian_kernel"]

@@ -82,11 +82,12 @@ class ResUNet(nn.Module):
 
 class ZUpdateResUNet(nn.Module):
     """Z step: ``z = ResUNet((x + u1).float())`` (runtime ``Z_Update_ResUNet`` at
-    ``models/Unrolled_ADMM.py:349-357``).  The attribute is ``net`` so keys read ``Z.net.*``."""
+    ``models/Unrolled_ADMM.py:349-357``; ``nc=(32, 64, 128, 256)`` for ``ZUpdateResUNet`` of
+    ``models/unrolled_admm_gaussian.py:74-82``).  The attribute is ``net`` so keys read ``Z.net.*``."""
 
-    def __init__(self):
+    def __init__(self, nc=(64, 128, 256, 512)):
         super().__init__()
-        self.net = ResUNet()
+        self.net = ResUNet(nc=tuple(nc))
 
     def forward(self, z):
         return self.net(z.float())
@@ -146,14 +147,19 @@ class SubNet(nn.Module):
     which is 1 small FFT per forward and is off the hot path.
     """
 
-    def __init__(self, n):
+    def __init__(self, n, n_out=None, shift=False):
+        """``n_out`` MLP outputs (default 2n: rho1 and rho2 per iteration; n for the single rho of
+        ``models/unrolled_admm_gaussian.py:43-71``, which returns [N,1,1,n]); ``shift``: that
+        variant's ``fft2(ifftshift(k_pad))`` in the PyTorch path (|.|^2 is shift invariant)."""
         super().__init__()
         self.n = n
+        self.n_out = 2 * n if n_out is None else n_out
+        self.shift = shift
         self.conv_layers = nn.Sequential(_Down(1, 4), _Down(4, 8), _Down(8, 16), _Down(16, 16))
         self.use_engine = True  # ROCm + eval: fused HIP feature extractor (gd_subnet_features)
         self.mlp = nn.Sequential(nn.Linear(16 * 8 * 8 + 1, 64), nn.ReLU(inplace=True),
                                  nn.Linear(64, 64), nn.ReLU(inplace=True),
-                                 nn.Linear(64, 2 * n), nn.Softplus())
+                                 nn.Linear(64, self.n_out), nn.Softplus())
 
     def _packed_params(self):
         """Folded conv+BN weights of the 8 convs in gd_subnet_features order: per layer w then b."""
@@ -196,10 +202,15 @@ class SubNet(nn.Module):
             h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
             w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2
             k_pad = F.pad(kernel, (w1, w2, h1, h2), "constant", 0)
-            Hk = torch.fft.fftn(k_pad, dim=[2, 3])
+            if self.shift:
+                Hk = torch.fft.fft2(torch.fft.ifftshift(k_pad, dim=(-2, -1)))
+            else:
+                Hk = torch.fft.fftn(k_pad, dim=[2, 3])
             feat = self.conv_layers((torch.abs(Hk) ** 2).float())
         feat = torch.cat((feat.view(N, 1, 16 * 8 * 8), alpha.float().view(N, 1, 1)), dim=2)
         out = self.mlp(feat) + 1e-6
+        if self.n_out == self.n:
+            return out.view(N, 1, 1, self.n)
         rho1 = out[:, :, 0:self.n].view(N, 1, 1, self.n)
         rho2 = out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
         return rho1, rho2

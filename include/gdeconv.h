@@ -24,6 +24,9 @@
  *   gd_richardson_lucy  models/Richard_Lucy.py:10-24 Richard_Lucy(n_iters).forward(y, psf)
  *   gd_tikhonov         models/Tikhonet.py:15-31     Tikhonov(filter).forward(y, psf, alpha, lam)
  *   gd_filter_power     models/Tikhonet.py:26-27     LtL = |psf_to_otf(laplacian_kernel(), y.size())|^2
+ *   gd_gx_init          models/unrolled_admm_gaussian.py:111-127  UnrolledADMMGaussian Y, H, init_l2
+ *   gd_gx_xupdate       models/unrolled_admm_gaussian.py:85-93 (+ dual update :145, denoiser input :142)
+ *   gd_gx_xupdate_backward  adjoint of XUpdateGaussian (autograd for train.py:41's model)
  */
 #ifndef GDECONV_H
 #define GDECONV_H
@@ -107,6 +110,30 @@ int gd_tikhonov(const float* y, const float* psf, long long psf_gstride, int h, 
 /* power_half[g][kx][ky] = |FFT2(filt[g])|^2 over the half spectrum (filt: real images [N][H][W],
  * any placement, e.g. the circularly shifted Laplacian of the reference's psf_to_otf). */
 int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, void* ws, void* stream);
+
+/* UnrolledADMMGaussian (the variant train.py trains): images H x W (H = W in {32, 48, 64, 128}) and
+ * PSFs of the SAME size, zero-padded to the 2H x 2W grid (pad_double) with the reference's
+ * ifftshift / fftshift / crop_half expressed as origin placement (the shift is a common phase that
+ * cancels).  state: gd_gx_state_bytes - |H|^2 and G = F(max(y,0)) conj(H) on the 2H grid, written
+ * by gd_gx_init, which also writes z0 = init_l2 (H x W).  ws: gd_workspace_bytes(N, 2H, 2W).
+ *
+ * gd_gx_xupdate: x = XUpdateGaussian(Y, Ht, HtH, z, u, rho) (H x W).  u may be NULL (zero).  If
+ *   x_prev != NULL, first u = u + rho_prev (x_prev - z) in place (the dual update of the previous
+ *   iteration, fused).  zin != NULL: also writes rho x + u (the next denoiser input).  xspec != NULL
+ *   (gd_gx_spec_bytes): saves the X spectrum for the backward.
+ * gd_gx_xupdate_backward: given dL/dx, writes dL/dz = rho M g, dL/du = -M g (M = the X update's
+ *   linear part, self-adjoint) and per-(galaxy, kx) parts of dL/drho [N][W+1] (sum them per galaxy);
+ *   z is the forward's z, xspec the forward's saved spectrum. */
+size_t gd_gx_state_bytes(int N, int H, int W);
+size_t gd_gx_spec_bytes(int N, int H, int W);
+int gd_gx_init(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+               long long alpha_stride, int N, int H, int W, void* state, float* z0, void* ws, void* stream);
+int gd_gx_xupdate(const float* z, float* u, const float* x_prev, const float* rho, long long rho_stride,
+                  const float* rho_prev, long long rho_prev_stride, float* x, float* zin, void* xspec,
+                  int N, int H, int W, void* state, void* ws, void* stream);
+int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho, long long rho_stride,
+                           const void* xspec, float* grad_z, float* grad_u, float* grad_rho_part, int N, int H,
+                           int W, void* state, void* ws, void* stream);
 
 /* SubNet feature extractor (models/Unrolled_ADMM.py:77-84): from the 128x128 half-spectrum OTF
  * of the PSFs (gd_psf_to_otf with H = W = 128; |OTF|^2 = |FFT2(pad128(psf))|^2), MaxPool2 and the

@@ -22,6 +22,8 @@ Reference call sites followed (paths relative to the reference root):
   wiener              models/Wiener.py:10-20
   richardson_lucy     models/Richard_Lucy.py:10-24
   tikhonov            models/Tikhonet.py:15-31 (+ laplacian_kernel, utils/utils_torch.py:95-99)
+  gx_*                models/unrolled_admm_gaussian.py:85-152 (UnrolledADMMGaussian; pad_double /
+                      crop_half utils/utils_torch.py:11-18)
 """
 import torch
 
@@ -158,6 +160,63 @@ def tikhonov(y, psf, alpha, lam, filt="Identity"):
     return torch.real(torch.fft.ifftn(numerator / divisor, dim=[2, 3]))
 
 
+def pad_double(img):
+    """utils/utils_torch.py:11-13."""
+    H, W = img.shape[-2], img.shape[-1]
+    return torch.nn.functional.pad(img, (W // 2, W // 2, H // 2, H // 2))
+
+
+def crop_half(img):
+    """utils/utils_torch.py:16-18."""
+    H, W = img.shape[-2], img.shape[-1]
+    return img[:, :, H // 4:3 * H // 4, W // 4:3 * W // 4]
+
+
+def gx_spectra(y, kernel):
+    """models/unrolled_admm_gaussian.py:118-123: max(y,0), Y, H, Ht, HtH on the 2x padded grid."""
+    fs = torch.fft
+    y = torch.maximum(y, torch.zeros_like(y))
+    Y = fs.fft2(fs.ifftshift(pad_double(y), dim=(-2, -1)))
+    H = fs.fft2(fs.ifftshift(pad_double(kernel), dim=(-2, -1)))
+    return y, Y, torch.conj(H), torch.abs(H) ** 2
+
+
+def gx_init_l2(Y, Ht, HtH, alpha):
+    """models/unrolled_admm_gaussian.py:111-115."""
+    rhs = Y * Ht
+    lhs = HtH + (1 / alpha)
+    x0 = torch.fft.fftshift(torch.fft.ifft2(rhs / lhs), dim=(-2, -1)).real
+    return crop_half(x0)
+
+
+def gx_x_update(Y, Ht, HtH, z, u, rho):
+    """models/unrolled_admm_gaussian.py:89-93 (XUpdateGaussian.forward)."""
+    fs = torch.fft
+    lhs = rho + HtH
+    rhs = Ht * Y + fs.fft2(fs.ifftshift(pad_double(rho * z - u), dim=(-2, -1)))
+    x = fs.fftshift(fs.ifft2(rhs / lhs), dim=(-2, -1)).real
+    return crop_half(x)
+
+
+def gx_forward(y, kernel, alpha, rho_iters, denoise=None, trace=None):
+    """models/unrolled_admm_gaussian.py:117-152 with the rhos given: [N,1,1,n] (SubNet) or [n].
+    Returns z_n (the last denoiser output); ``trace`` receives x, z, u, rho lists (analysis=True)."""
+    denoise = denoise if denoise is not None else (lambda t: t)
+    y, Y, Ht, HtH = gx_spectra(y, kernel)
+    z = gx_init_l2(Y, Ht, HtH, alpha)
+    u = torch.zeros_like(y)
+    n_iters = rho_iters.shape[-1]
+    for i in range(n_iters):
+        rho = rho_iters[:, :, :, i].view(-1, 1, 1, 1) if rho_iters.dim() == 4 else rho_iters[i]
+        x = gx_x_update(Y, Ht, HtH, z, u, rho)
+        z = denoise(rho * x + u)
+        u = u + rho * (x - z)
+        if trace is not None:
+            for k, t in (("x", x), ("z", z), ("u", u), ("rho", rho)):
+                trace.setdefault(k, []).append(t)
+    return z
+
+
 def normwise_error(out, ref):
     """Per-galaxy max|out - ref| / max|ref| (the parity metric of SURVEY.md 8(d)); returns [N]."""
     out = out.detach().double().cpu().reshape(out.shape[0], -1)
@@ -167,4 +226,5 @@ def normwise_error(out, ref):
 
 __all__ = ["psf_to_otf", "conv_fft_batch", "x_update", "v_update_poisson", "v_update_gaussian",
            "init_l2", "admm_forward", "wiener", "richardson_lucy", "tikhonov", "laplacian_kernel",
+           "pad_double", "crop_half", "gx_spectra", "gx_init_l2", "gx_x_update", "gx_forward",
            "normwise_error"]

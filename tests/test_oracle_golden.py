@@ -131,3 +131,65 @@ def test_tikhonet_full_model(filt):
         x = O.tikhonov(torch.max(obs, torch.zeros_like(obs)), psf, alpha, torch.tensor(1.0), filt)
         out = m.denoiser(x) * alpha
     assert torch.equal(out, T(g[f"tikhonet_{filt}_48"]))
+
+
+def _gauss2x_nets(n):
+    """Host-side SubNet (n outputs, ifftshift) + ResUNet(nc=32..256) with the fixture weights."""
+    from gdeconv.nets import SubNet, ZUpdateResUNet
+    from gdeconv.weights import make_state_dict
+
+    class M(torch.nn.Module):  # module tree of the reference UnrolledADMMGaussian (X has no params)
+        def __init__(self):
+            super().__init__()
+            self.Z = ZUpdateResUNet(nc=(32, 64, 128, 256))
+            self.init = SubNet(n, n_out=n, shift=True)
+
+    m = M()
+    m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    m.init.set_fold_bn(False)
+    return m.eval()
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_gauss2x_full_model(n):
+    """UnrolledADMMGaussian (models/unrolled_admm_gaussian.py:96-152): oracle + host nets, traces."""
+    torch.set_num_threads(8)
+    g = golden("gauss2x.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    m = _gauss2x_nets(n)
+    with torch.no_grad():
+        rho = m.init(psf, alpha)
+        assert torch.equal(rho, T(g[f"full_n{n}_rho"]))
+        tr = {}
+        out = O.gx_forward(obs, psf, alpha, rho, denoise=m.Z, trace=tr)
+    assert torch.equal(out, T(g[f"full_n{n}_out"]))
+    for k in ("x", "z", "u"):
+        assert torch.equal(torch.stack(tr[k]), T(g[f"full_n{n}_{k}"]))
+
+
+def test_gauss2x_identity_and_sizes():
+    g = golden("gauss2x.npz")
+    out = O.gx_forward(T(g["obs"]), T(g["psf"]), T(g["alpha"]), T(g["id_n8_rho"]))
+    assert torch.equal(out, T(g["id_n8_out"]))
+    for L in (32, 64):
+        out = O.gx_forward(T(g[f"id{L}_obs"]), T(g[f"id{L}_psf"]), T(g[f"id{L}_alpha"]), T(g[f"id{L}_rho"]))
+        assert torch.equal(out, T(g[f"id{L}_out"]))
+
+
+def test_gauss2x_gradients():
+    """Autograd through the oracle reproduces the reference's gradients (training path, train.py:41)."""
+    torch.set_num_threads(8)
+    g = golden("gauss2x.npz")
+    obs, psf, alpha, R = T(g["obs"]), T(g["psf"]), T(g["alpha"]), T(g["R"])
+    rho = T(g["grad_rho_iters"]).clone().requires_grad_(True)
+    out = O.gx_forward(obs, psf, alpha, rho)
+    (out * R).sum().backward()
+    assert torch.equal(out.detach(), T(g["grad_rho_iters_out"]))
+    assert torch.equal(rho.grad, T(g["grad_rho_iters_grad"]))
+    m = _gauss2x_nets(2)
+    out = O.gx_forward(obs, psf, alpha, m.init(psf, alpha), denoise=m.Z)
+    (out * R).sum().backward()
+    params = dict(m.named_parameters())
+    assert torch.equal(out.detach(), T(g["grad_full_out"]))
+    for k in ("init.mlp.4.weight", "init.mlp.4.bias", "Z.net.m_tail.weight", "Z.net.m_head.weight"):
+        assert torch.equal(params[k].grad, T(g[f"grad_full_{k}"])), k
