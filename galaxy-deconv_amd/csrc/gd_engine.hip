@@ -1056,6 +1056,27 @@ __global__ __launch_bounds__((RowGeo<L, 1, RBX>::THREADS)) void k_row_invfwd(Arg
     split_store<L, R>(a, lds, g, row0, tid);
 }
 
+// ---------------------------------------------------------------- sparse filter power
+// |L(kx, ky)|^2 of a filter image with few non-zero taps (the Tikhonov Laplacian), by direct DFT in
+// double: sum_t v_t exp(-2 pi i (ky r_t + kx c_t) / L), rounded once.  The regulariser divides the
+// spectrum where |H|^2 is ~0, so its absolute error matters there; an fp32 FFT of the placed 3x3
+// stencil carries ~1e-6 absolute error, this carries none beyond the final rounding.
+__global__ __launch_bounds__(256) void k_sparse_power(const int* rc, const float* vals, int ntaps, float* out,
+                                                      int L, int K) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= K * L) return;
+    const int kx = idx / L, ky = idx - kx * L;
+    double re = 0.0, im = 0.0;
+    for (int t = 0; t < ntaps; ++t) {
+        const long long ph = ((long long)ky * rc[2 * t] + (long long)kx * rc[2 * t + 1]) % L;  // exact phase index
+        double sn, cs;
+        sincospi(-2.0 * double(ph) / double(L), &sn, &cs);
+        re += double(vals[t]) * cs;
+        im += double(vals[t]) * sn;
+    }
+    out[idx] = float(re * re + im * im);
+}
+
 // ---------------------------------------------------------------- host-side launch helpers
 thread_local std::string g_last_error;
 
@@ -1707,6 +1728,16 @@ int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho
     a.s_w = reinterpret_cast<float2*>(const_cast<void*>(xspec));
     a.o0 = grad_z; a.o1 = grad_u; a.o2 = grad_rho_part;
     return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_x_bwd(a, (hipStream_t)stream); });
+}
+
+int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
+                         void* stream) {
+    if (H != W || H <= 0 || H > 4096) return fail(GD_ERR_UNSUPPORTED, "square images only");
+    if (ntaps < 0 || (ntaps > 0 && (!rc || !vals))) return fail(GD_ERR_ARG, "bad tap list");
+    const int K = W / 2 + 1;
+    hipLaunchKernelGGL(k_sparse_power, dim3((K * H + 255) / 256), dim3(256), 0, (hipStream_t)stream, rc, vals, ntaps,
+                       power_half, H, K);
+    return check_launch("k_sparse_power");
 }
 
 int gd_profile_enable(int level) {

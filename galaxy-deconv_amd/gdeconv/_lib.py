@@ -41,6 +41,7 @@ SIGNATURES = {
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
     "gd_tikhonov": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_filter_power": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "gd_filter_power_taps": (_I, [_P, _P, _I, _P, _I, _I, _P]),
     "gd_gx_state_bytes": (_SZ, [_I, _I, _I]),
     "gd_gx_spec_bytes": (_SZ, [_I, _I, _I]),
     "gd_gx_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _I, _I, _I, _P, _P, _P, _P]),

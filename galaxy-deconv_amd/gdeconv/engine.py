@@ -173,6 +173,22 @@ def filter_power(filt):
     return out
 
 
+def filter_power_taps(filt_img, device):
+    """|FFT2|^2 over the half spectrum [1, W//2+1, H] of ONE sparse filter image (e.g. the placed
+    Laplacian) by direct DFT in double on the device (gd_filter_power_taps).  The tap list of the
+    constant image is extracted on the host (parameter setup, like weights)."""
+    lib = _lib.load()
+    img = filt_img.detach().reshape(filt_img.shape[-2], filt_img.shape[-1]).float().cpu()
+    H, W = img.shape
+    nz = torch.nonzero(img)
+    rc = nz.to(torch.int32).contiguous().to(device)
+    vals = img[nz[:, 0], nz[:, 1]].contiguous().to(device)
+    out = torch.empty(1, W // 2 + 1, H, dtype=torch.float32, device=device)
+    _lib.check(lib.gd_filter_power_taps(rc.data_ptr() if len(nz) else None, vals.data_ptr() if len(nz) else None,
+                                        int(len(nz)), out.data_ptr(), H, W, _stream()), "gd_filter_power_taps")
+    return out
+
+
 def tikhonov(y, psf, alpha, lam, ltl=None):
     """models/Tikhonet.py:15-31 (Tikhonov.forward) on the HIP engine: Re IFFT2(conj(H) FFT2(y/alpha) /
     (|H|^2 + lam LtL)); ``ltl`` None = filter 'Identity', else a half-spectrum [1|N, W//2+1, H]."""
@@ -240,9 +256,13 @@ class GaussXState:
         self.ws = torch.empty(int(self.lib.gd_workspace_bytes(N1, 2 * self.H, 2 * self.W)), dtype=torch.uint8,
                               device=dev)
         self.spec_bytes = int(self.lib.gd_gx_spec_bytes(N1, self.H, self.W))
+        self.z0 = self._init()   # the state is valid from construction on
 
     def init(self):
-        """z0 = init_l2(Y, Ht, HtH, alpha) (:111-115)."""
+        """z0 = init_l2(Y, Ht, HtH, alpha) (:111-115), computed with the state at construction."""
+        return self.z0
+
+    def _init(self):
         z0 = torch.empty_like(self.y)
         k = self.psf
         _lib.check(self.lib.gd_gx_init(self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3],
@@ -387,5 +407,5 @@ class ADMMState:
 
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
-           "tikhonov", "filter_power", "GaussXState", "gx_x_update",
+           "tikhonov", "filter_power", "filter_power_taps", "GaussXState", "gx_x_update",
            "ADMMState", "workspace", "empty_otf", "supported", "subnet_features"]

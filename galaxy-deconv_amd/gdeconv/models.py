@@ -177,7 +177,8 @@ def placed_filter(ker, H, W, device):
 
 class Tikhonov(nn.Module):
     """models/Tikhonet.py:8-31: x = Re IFFT2(conj(H) FFT2(y/alpha) / (|H|^2 + lam [|L|^2])).  The
-    Laplacian's |L|^2 is computed on the device once per (size, device) and cached."""
+    Laplacian's |L|^2 is computed on the device once per (size, device) by direct DFT in double over
+    its 7 taps (gd_filter_power_taps) and cached."""
 
     def __init__(self, filter="Identity"):
         super().__init__()
@@ -191,7 +192,7 @@ class Tikhonov(nn.Module):
     def ltl(self, H, W, device):
         key = (H, W, str(device))
         if key not in self._ltl:
-            self._ltl[key] = engine.filter_power(placed_filter(self.lap, H, W, device))
+            self._ltl[key] = engine.filter_power_taps(placed_filter(self.lap, H, W, "cpu"), device)
         return self._ltl[key]
 
     def forward(self, y, psf, alpha, lam):

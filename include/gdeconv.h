@@ -111,6 +111,12 @@ int gd_tikhonov(const float* y, const float* psf, long long psf_gstride, int h, 
  * any placement, e.g. the circularly shifted Laplacian of the reference's psf_to_otf). */
 int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, void* ws, void* stream);
 
+/* Same for ONE filter given as ntaps non-zero pixels (rc = [row, col] pairs in [0,H) x [0,W), vals),
+ * by direct DFT in double rounded once - for the sparse Tikhonov Laplacian, whose |L|^2 sits in the
+ * divisor where |H|^2 vanishes (fp32 FFT rounding would be amplified there). */
+int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
+                         void* stream);
+
 /* UnrolledADMMGaussian (the variant train.py trains): images H x W (H = W in {32, 48, 64, 128}) and
  * PSFs of the SAME size, zero-padded to the 2H x 2W grid (pad_double) with the reference's
  * ifftshift / fftshift / crop_half expressed as origin placement (the shift is a common phase that
