@@ -121,7 +121,7 @@ def parse():
     p.add_argument("--chunk-mb", type=float, default=None,
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
-    p.add_argument("--fused", type=int, default=None, help="1: one-kernel Gaussian iteration (256^2), 0: three kernels")
+    p.add_argument("--fused", type=int, default=None, help="2: one-kernel Gaussian iteration with register transposes, 1: one-kernel with parking (256^2), 0: three kernels")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
     return p.parse_args()
@@ -280,7 +280,9 @@ def main():
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
                    "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
-                   "iteration": "fused (k_gal_iter, one workgroup per galaxy)" if use_fused else "three-kernel"},
+                   "iteration": ({1: "fused (k_gal_iter, one workgroup per galaxy)",
+                                  2: "fused (k_gal_iter2, register transpose, one workgroup per galaxy)"}[fused]
+                                 if use_fused else "three-kernel")},
         "roofline": roofline,
         "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},

@@ -883,6 +883,185 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     });
 }
 
+// No-park variant (gd_set_fused_iteration(2)): the column transforms use the register (DPP) transpose,
+// so S can hold slice B's bins while column A is transformed, and column A's results go to S (rows of
+// the first half) or stay in registers (second half) while column B is processed.  Nothing round-trips
+// through global memory: the iteration moves exactly its algorithmic 7.5 words per pixel (k_gal_iter
+// adds 2 x 131 KiB of parked registers per galaxy, ~21 % of its fabric traffic).
+template <int L, bool FIRST, bool LAST>
+__global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
+    using FG = FusedGeo<L>;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    static_assert(F1 == 16 && F2 == 16, "register transpose: 16 x 16 lines");
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
+    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
+    __shared__ float2 nyqx[L];      // line 0's packed column 0 / Nyquist spectrum (S holds slice B)
+    __shared__ float nyqo[L];       // x(., L/2)
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * FG::XCH;
+    fill_twiddles<L>(tw, tid, FG::THREADS);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    GD_TRACE(0);
+
+    // R: pair p = line + LINES q, row FFTs with the LDS exchange (S is free)
+    float2 X[FG::PPL][F2];
+    {
+        const float* z = a.a0 + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+        }
+    }
+    __syncthreads();  // twiddles
+    GD_TRACE(1);
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
+    lds_barrier();  // exchange areas -> slice A
+    GD_TRACE(2);
+
+    // A: bins of columns 0..KS-1 and the Nyquist bins
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        const int p = line + LINES * q;
+        float2* row = S + p * SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = j + F1 * r;
+            if (r < KS / F1) row[k] = X[q][r];
+            if (r == 0 && j == 0) row[KS] = X[q][r];
+            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];
+            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];
+        }
+    }
+    lds_barrier();
+    float2 C[F2];
+    fused_gather<L>(S, line, j, C);
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int y = j + F1 * s;
+        const float2 w = nyq[y >> 1];
+        if (l0) C[s].y = (y & 1) ? w.y : w.x;
+    }
+    lds_barrier();  // slice A read -> slice B
+    GD_TRACE(3);
+    // B's bins -> S straight from the row registers (X dies here)
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        float2* row = S + (line + LINES * q) * SLD;
+#pragma unroll
+        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
+            const int k = j + F1 * r;
+            if (r < 2 * KS / F1) row[k - KS] = X[q][r];
+            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
+                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // X dies here: keep its LDS stores ahead of column A's FFT
+    GD_TRACE(4);
+
+    // column A in registers (S is occupied by slice B); columns 0 and L/2 ride together in line 0
+    line_fft<L, false, true, true>(C, opaque(j), nullptr, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqx[j + F1 * s] = C[s];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int ky = j + F1 * s;
+            const float2 z = C[s], zm = nyqx[(L - ky) & (L - 1)];
+            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        }
+    }
+    lds_barrier();  // nyqc complete; slice B complete in S
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
+        nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
+                                                 true, inv_n);
+    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n);
+    lds_barrier();  // Nyquist results
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const float2 cn = nyqc[j + F1 * s];
+        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
+    }
+    line_fft<L, true, true, true>(C, opaque(j), nullptr, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
+    }
+    GD_TRACE(5);
+
+    // B: gather, then column A's first-half rows -> S (row layout [yl][SLD], A at [line])
+    float2 Cb[F2];
+    fused_gather<L>(S, line, j, Cb);
+    lds_barrier();  // slice B read -> row half spectra
+    GD_TRACE(6);
+#pragma unroll
+    for (int s = 0; s < F2 / 2; ++s) {
+        float2* rr = S + (j + F1 * s) * SLD;
+        rr[line] = make_float2(C[s].x, l0 ? 0.f : C[s].y);  // column 0: real part (irfft)
+    }
+    __builtin_amdgcn_sched_barrier(0);  // C's first half dies here
+    line_fft<L, false, true, true>(Cb, opaque(j), nullptr, tw);
+    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n);
+    line_fft<L, true, true, true>(Cb, opaque(j), nullptr, tw);
+    GD_TRACE(7);
+
+    // I: half hf = rows [hf L/2, (hf+1) L/2): row IFFT of the packed pairs, store
+    float* out = a.o0 + (size_t)g * L * L;
+    static_for<0, 2>([&](auto hfc) {
+        constexpr int hf = decltype(hfc)::value;
+        if constexpr (hf == 1) {
+            lds_barrier();  // exchange areas -> row half spectra
+#pragma unroll
+            for (int s = F2 / 2; s < F2; ++s) {
+                float2* rr = S + (j + F1 * s - L / 2) * SLD;
+                rr[line] = make_float2(C[s].x, l0 ? 0.f : C[s].y);
+            }
+        }
+#pragma unroll
+        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) S[(j + F1 * s - hf * L / 2) * SLD + KS + line] = Cb[s];
+        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        lds_barrier();
+        float2 V[F2];
+        {
+            const int jj = opaque(j);
+            const float2* re = S + (2 * opaque(line)) * SLD;
+            const float2* ro = re + SLD;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                const int k = jj + F1 * r;
+                float2 be, bo;
+                if (k <= L / 2) {
+                    be = re[k];
+                    bo = ro[k];
+                } else {
+                    be = cconj(re[L - k]);
+                    bo = cconj(ro[L - k]);
+                }
+                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+        lds_barrier();  // row half spectra -> exchange areas
+        line_fft<L, true, true>(V, j, my, tw);
+        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            o[F1 * r] = V[r].x;
+            o[L + F1 * r] = V[r].y;
+        }
+        GD_TRACE(8 + hf);
+    });
+}
+
 // ---------------------------------------------------------------- RI: row inverse + sink
 template <int MODE>
 struct RiTraits {
@@ -1085,6 +1264,7 @@ constexpr const char* kColName = "k_col";
 constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
 constexpr const char* kGalIterName = "k_gal_iter";
+constexpr const char* kGalIter2Name = "k_gal_iter2";
 
 inline int fail(int code, const char* msg) {
     g_last_error = msg;
@@ -1183,7 +1363,17 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_iter");
     }
-    static int gal_iter(const Args& a, hipStream_t st) {
+    template <bool FIRST, bool LAST>
+    static int gal_iter2_v(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalIter2Name, FIRST + 2 * LAST), st);
+        hipLaunchKernelGGL((k_gal_iter2<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_iter2");
+    }
+    static int gal_iter(const Args& a, hipStream_t st, int variant) {
+        if (variant == 2) {
+            if (a.first) return a.last ? gal_iter2_v<true, true>(a, st) : gal_iter2_v<true, false>(a, st);
+            return a.last ? gal_iter2_v<false, true>(a, st) : gal_iter2_v<false, false>(a, st);
+        }
         if (a.first) return a.last ? gal_iter_v<true, true>(a, st) : gal_iter_v<true, false>(a, st);
         return a.last ? gal_iter_v<false, true>(a, st) : gal_iter_v<false, false>(a, st);
     }
@@ -1352,7 +1542,7 @@ struct Ops {
     static int admm_iter_gauss(Args a, hipStream_t st0) {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
         if constexpr (has_fused<L>()) {
-            if (g_fused) return Lc::gal_iter(a, st0);  // one pass, no workspace
+            if (g_fused) return Lc::gal_iter(a, st0, g_fused);  // one pass, no workspace
         }
         return for_chunks(a, L, st0, [&](const Args& b, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_ONE>(b, st));
@@ -1796,7 +1986,7 @@ int gd_set_pipeline_streams(int streams) {
 
 int gd_set_fused_iteration(int on) {
     const int old = g_fused;
-    g_fused = on ? 1 : 0;
+    g_fused = (on == 1 || on == 2) ? on : 0;
     return old;
 }
 

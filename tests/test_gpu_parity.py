@@ -117,9 +117,10 @@ def _spectral_model(n, llh, dev, rho1, rho2):
     return m
 
 
-@pytest.fixture(params=[1, 0], ids=["fused", "three_kernel"])
+@pytest.fixture(params=[2, 1, 0], ids=["fused_regs", "fused", "three_kernel"])
 def fused(request):
-    """Gaussian iterations through the one-kernel whole-galaxy path (256^2) or the three-kernel path."""
+    """Gaussian iterations through the one-kernel whole-galaxy path (256^2; 2: register-transpose
+    k_gal_iter2, 1: parking k_gal_iter) or the three-kernel path."""
     from gdeconv import _lib
     lib = _lib.load()
     old = lib.gd_set_fused_iteration(request.param)
@@ -137,8 +138,9 @@ def test_admm256_spectral_engine(dev, llh, fused):
     assert nerr(out, T(g[f"{llh}_out"])) < TOL
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("n", [1, 2, 3])
-def test_fused_iteration_matches_three_kernel_path(dev, n):
+def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
     """k_gal_iter (first / middle / last variants) against the three-kernel path and the oracle, with
     per-galaxy rho and a ragged batch."""
     from gdeconv import _lib
@@ -150,7 +152,7 @@ def test_fused_iteration_matches_three_kernel_path(dev, n):
     rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
     rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
     m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
-    old = lib.gd_set_fused_iteration(1)
+    old = lib.gd_set_fused_iteration(variant)
     try:
         with torch.no_grad():
             out_f = m(obs, psf, alpha).cpu()

@@ -33,6 +33,7 @@ float time_ms(F&& f, int reps = 10) {
 
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096;
+    const int variant = argc > 2 ? atoi(argv[2]) : 1;  // 1: k_gal_iter (parking), 2: k_gal_iter2 (register transpose)
     constexpr int L = 256, K = L / 2 + 1;
     const size_t img = (size_t)N * L * L, spec = (size_t)N * K * L;
     float *z, *zin, *par;
@@ -57,16 +58,27 @@ int main(int argc, char** argv) {
 #endif
     const double img_b = L * L * 4.0, half_b = K * L * 8.0;
     const double gb_mid = N * (2 * img_b + 5.5 * half_b) / 1e9;
-    float t = time_ms([&] { hipLaunchKernelGGL((k_gal_iter<L, false, false>), dim3(N), dim3(1024), 0, 0, a); });
-    printf("k_gal_iter<256,MID>  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", t, gb_mid / t, gb_mid);
+    auto launch = [&] {
+        if (variant == 2)
+            hipLaunchKernelGGL((k_gal_iter2<L, false, false>), dim3(N), dim3(1024), 0, 0, a);
+        else
+            hipLaunchKernelGGL((k_gal_iter<L, false, false>), dim3(N), dim3(1024), 0, 0, a);
+    };
+    float t = time_ms(launch);
+    printf("%s<256,MID>  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", variant == 2 ? "k_gal_iter2" : "k_gal_iter", t,
+           gb_mid / t, gb_mid);
 #if GD_FUSED_TRACE
-    hipLaunchKernelGGL((k_gal_iter<L, false, false>), dim3(N), dim3(1024), 0, 0, a);
+    launch();
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> h((size_t)N * 16);
     CK(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
-    const char* names[] = {"start -> z loaded", "row FFTs + park B bins", "slice A bins -> LDS", "gather A",
+    const char* names1[] = {"start -> z loaded", "row FFTs + park B bins", "slice A bins -> LDS", "gather A",
                            "column A (+ Nyquist) + park A", "unpark B, bins -> LDS", "gather B",
                            "column B + I half 0", "I half 1"};
+    const char* names2[] = {"start -> z loaded", "row FFTs", "slice A bins -> LDS + gather A",
+                            "slice B bins -> LDS", "column A (+ Nyquist), regs", "gather B",
+                            "A rows half 0 + column B", "I half 0", "I half 1"};
+    const char** names = variant == 2 ? names2 : names1;
     const int NP = 10;
     double sum[NP] = {0};
     unsigned long long t0 = ~0ull, t1 = 0;
