@@ -312,6 +312,51 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI, RBX>::THREADS)) void
     split_store<L, R>(a, lds, g, row0, tid);
 }
 
+// ---------------------------------------------------------------- PSF row spectra (init)
+// psf_to_otf's row transform (utils/utils_torch.py:84-91), restricted to the h non-zero rows of the
+// circularly shifted, zero-padded PSF: psf row i sits in padded row (i - h/2) mod L and its pixel jj in
+// padded column (jj - h/2) mod L.  Rows 2p, 2p+1 ride one complex line (same image: the packing
+// rule), split after the FFT and stored compactly as P[kx][i] (i < h, contiguous) in T slot 1, where
+// k_col<C_G_INIT> picks its OTF column up with a few coalesced loads.
+template <int L>
+__global__ __launch_bounds__(256) void k_psf_rows(Args a) {
+    using G = Geo<L>;
+    constexpr int F1 = G::F1, F2 = G::F2, LPB = G::LPB, K = G::K;
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 lds[cmax(LPB * G::RLD, LPB * G::XCH)];
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int h = a.h, c0 = h >> 1, pairs = h >> 1;
+    const int blocks_per_g = (pairs + LPB - 1) / LPB;
+    const int g = blockIdx.x / blocks_per_g;
+    const int p0 = (blockIdx.x - g * blocks_per_g) * LPB;
+    fill_twiddles<L>(tw, tid, 256);
+    const int p = p0 + line;
+    const float* ps = a.psf + (long long)g * a.psf_gstride + (long long)(2 * p) * h;
+    float2 v[F2];
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        int jj = j + F1 * s + c0;
+        if (jj >= L) jj -= L;
+        v[s] = (p < pairs && jj < h) ? make_float2(ps[jj], ps[h + jj]) : make_float2(0.f, 0.f);
+    }
+    __syncthreads();  // twiddles
+    line_fft<L, false>(v, j, lds + line * G::XCH, tw);
+    __syncthreads();  // exchange areas -> row buffer
+#pragma unroll
+    for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
+    __syncthreads();
+    float2* P = a.T + tidx(g, 1, 0, 0, K, L);
+    for (int idx = tid; idx < LPB * K; idx += 256) {
+        const int m = idx % LPB, k = idx / LPB;
+        if (p0 + m >= pairs) continue;
+        const float2 C = lds[m * G::RLD + k];
+        const float2 D = lds[m * G::RLD + (k == 0 ? 0 : L - k)];
+        // row 2p: (C + conj D)/2 ; row 2p+1: (C - conj D)/(2i) -> adjacent: one 16-byte store
+        *reinterpret_cast<float4*>(P + (size_t)k * h + 2 * (p0 + m)) =
+            make_float4(0.5f * (C.x + D.x), 0.5f * (C.y - D.y), 0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+    }
+}
+
 // ---------------------------------------------------------------- C: column pass
 template <int MODE>
 struct ColTraits {
@@ -387,67 +432,18 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         line_fft<L, false>(P, j, my, tw);
         if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
     }
-    // C_G_INIT: the OTF column H(., kx) straight from the h x h PSF: row DFT at kx of the (at most h)
-    // non-zero rows of the circularly shifted, zero-padded PSF, then the column FFT.  The block first
-    // computes the row-DFT values S[i][line] for its LPB columns cooperatively (lanes of a 16-group
-    // share the PSF row i -> broadcast reads; no divergence), in the exchange area, optionally after
-    // the PSFs of the (at most NGB) galaxies it touches staged in LDS with rows padded to h+1.
+    // C_G_INIT: the OTF column H(., kx) from the PSF's row spectra P[kx][i] (k_psf_rows, T slot 1):
+    // padded row ky holds psf row i = (ky + h/2) mod L when i < h, zero otherwise; then the column FFT.
     float2 Hc[MODE == C_G_INIT ? F2 : 1];
     if constexpr (MODE == C_G_INIT) {
-        const int h = a.h, hp = h + 1, c0p = h >> 1;
-        constexpr int NGB = (G::LPB + K - 2) / K + 1;                  // galaxies a block can touch
-        const int gb = (blockIdx.x * G::LPB) / K;                      // first galaxy of the block
-        const int pst = (NGB * h * hp + 1) & ~1;                        // staged floats (even)
-        const bool staged = pst + 2 * G::LPB * h <= G::COL_LDS * 2;
-        float* pl = reinterpret_cast<float*>(xch);
-        float2* S = staged ? reinterpret_cast<float2*>(pl + pst) : xch;  // [h][LPB]
-        __syncthreads();  // (the forward FFT above used xch)
-        if (staged) {
-            const int ng = (a.N - gb < NGB) ? a.N - gb : NGB;
-            for (int q = tid; q < ng * h * h; q += 256) {
-                const int gg = q / (h * h), rem = q - gg * h * h, i = rem / h, jj = rem - i * h;
-                pl[(gg * h + i) * hp + jj] = a.psf[(long long)(gb + gg) * a.psf_gstride + rem];
-            }
-            __syncthreads();
-        }
-        const int cst = (L - c0p) % L;  // padded column of psf column 0
-        for (int o = tid; o < G::LPB * h; o += 256) {
-            const int i = o / G::LPB, ln = o - i * G::LPB;
-            const int fo = blockIdx.x * G::LPB + ln;
-            float2 acc0 = make_float2(0.f, 0.f), acc1 = acc0;
-            if (fo < a.N * K) {
-                const int go = fo / K, kxo = fo - go * K;
-                const float* row = staged ? pl + ((go - gb) * h + i) * hp
-                                          : a.psf + (long long)go * a.psf_gstride + (long long)i * h;
-                int idx = (kxo * cst) % L;   // twiddle index kx * c (mod L), c = column of jj
-                int jj = 0;
-                for (; jj + 1 < h; jj += 2) {  // two independent accumulators
-                    const float2 w0 = tw[idx];
-                    idx += kxo; if (idx >= L) idx -= L;
-                    const float2 w1 = tw[idx];
-                    idx += kxo; if (idx >= L) idx -= L;
-                    const float v0 = row[jj], v1 = row[jj + 1];
-                    acc0.x = fmaf(v0, w0.x, acc0.x);
-                    acc0.y = fmaf(v0, w0.y, acc0.y);
-                    acc1.x = fmaf(v1, w1.x, acc1.x);
-                    acc1.y = fmaf(v1, w1.y, acc1.y);
-                }
-                if (jj < h) {
-                    const float2 w0 = tw[idx];
-                    acc0.x = fmaf(row[jj], w0.x, acc0.x);
-                    acc0.y = fmaf(row[jj], w0.y, acc0.y);
-                }
-            }
-            S[i * G::LPB + ln] = cadd(acc0, acc1);
-        }
-        __syncthreads();
+        const int h = a.h, c0p = h >> 1;
+        const float2* Pr = a.T + tidx(g, 1, 0, 0, K, L) + (size_t)kx * h;
 #pragma unroll
         for (int s = 0; s < F2; ++s) {
             int i = j + F1 * s + c0p;
             if (i >= L) i -= L;
-            Hc[s] = (i < h) ? S[i * G::LPB + line] : make_float2(0.f, 0.f);
+            Hc[s] = (i < h) ? Pr[i] : make_float2(0.f, 0.f);
         }
-        __syncthreads();  // S -> exchange areas
         line_fft<L, false>(Hc, j, my, tw);
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
@@ -1260,6 +1256,7 @@ __global__ __launch_bounds__(256) void k_sparse_power(const int* rc, const float
 thread_local std::string g_last_error;
 
 constexpr const char* kRowFwdName = "k_row_fwd";
+constexpr const char* kPsfRowsName = "k_psf_rows";
 constexpr const char* kColName = "k_col";
 constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
@@ -1344,6 +1341,12 @@ struct Launcher {
         ProfScope ps(nm(kRowFwdName, MODE), st);
         hipLaunchKernelGGL((k_row_fwd<L, MODE>), dim3(row_grid<RfTraits<MODE>::NI>(a.N)), dim3(RowGeo<L, RfTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_fwd");
+    }
+    static int psf_rows(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kPsfRowsName, 0), st);
+        const int bpg = (a.h / 2 + G::LPB - 1) / G::LPB;
+        hipLaunchKernelGGL((k_psf_rows<L>), dim3(a.N * bpg), dim3(256), 0, st, a);
+        return check_launch("k_psf_rows");
     }
     template <int MODE>
     static int col(const Args& a, hipStream_t st) {
@@ -1532,6 +1535,7 @@ struct Ops {
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::template rf<RF_YA>(b, st));
+            GD_TRY(Lc::psf_rows(b, st));  // PSF row spectra -> slot 1 (free until RIF_CLAMP)
             GD_TRY(Lc::template col<C_G_INIT>(b, st));
             b.o0 = a.o2;    // RIF_CLAMP writes x0 -> zin and its row spectra -> slot 1
             b.t_slot = 1;
