@@ -379,28 +379,59 @@ struct ColTraits {
 //   V~   = (rho2' (|H|^2 X + U2~) + G) / (1 + rho2')               V step :335-336
 //   W~'  = V~ - U2~ ;  returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last iteration)
 // First iteration: U1 = 0 (not read); W~ = conj(H) V1 was written by the init (C_G_W1).
+#ifndef GD_RCP_DIV
+#define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % k_gal_iter time)
+#endif
+struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the variant skips them)
+    float hh;
+    float2 G, U1, W;
+};
 template <bool FIRST, bool LAST>
-__device__ __forceinline__ float2 gauss_iter_elem(const Args& a, size_t o, float2 Zk, float r1, float r2,
-                                                  float r2n, bool valid, float inv_n) {
-    const float hh = a.s_hh[o];
-    float2 U1 = make_float2(0.f, 0.f), Gk = make_float2(0.f, 0.f);
-    if constexpr (!LAST) Gk = a.s_g[o];
-    if constexpr (!FIRST) U1 = a.s_u1[o];
-    const float2 Wt = a.s_w[o];
+__device__ __forceinline__ GState gauss_load(const Args& a, size_t o) {
+    GState st;
+    st.hh = a.s_hh[o];
+    st.G = make_float2(0.f, 0.f);
+    st.U1 = make_float2(0.f, 0.f);
+    if constexpr (!LAST) st.G = a.s_g[o];
+    if constexpr (!FIRST) st.U1 = a.s_u1[o];
+    st.W = a.s_w[o];
+    return st;
+}
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 Zk, const GState& st, float r1,
+                                                float r2, float r2n, bool valid, float inv_n) {
+    const float hh = st.hh;
+    const float2 U1 = st.U1, Gk = st.G, Wt = st.W;
     const float lhs = r1 * hh + r2;
     const float2 A = csub(Zk, U1);
+#if GD_RCP_DIV
+    // one hardware reciprocal per bin (1 ulp) instead of two IEEE divisions; 1/(1 + rho2') per galaxy
+    const float rl = __builtin_amdgcn_rcpf(lhs);
+    const float2 X = make_float2((r1 * A.x + r2 * Wt.x) * rl, (r1 * A.y + r2 * Wt.y) * rl);
+#else
     const float2 X = make_float2((r1 * A.x + r2 * Wt.x) / lhs, (r1 * A.y + r2 * Wt.y) / lhs);
+#endif
     if constexpr (LAST) return cscale(X, inv_n);
     const float2 U1n = csub(cadd(U1, X), Zk);
     const float2 HHX = cscale(X, hh);
     const float2 U2t = csub(HHX, Wt);
     const float d = 1.0f + r2n;
+#if GD_RCP_DIV
+    const float rd = __builtin_amdgcn_rcpf(d);
+    const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) * rd, (r2n * (HHX.y + U2t.y) + Gk.y) * rd);
+#else
     const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
+#endif
     if (valid) {
         a.s_u1[o] = U1n;
         a.s_w[o] = csub(Vt, U2t);
     }
     return cscale(cadd(X, U1n), inv_n);
+}
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ float2 gauss_iter_elem(const Args& a, size_t o, float2 Zk, float r1, float r2,
+                                                  float r2n, bool valid, float inv_n) {
+    return gauss_iter_st<FIRST, LAST>(a, o, Zk, gauss_load<FIRST, LAST>(a, o), r1, r2, r2n, valid, inv_n);
 }
 
 // VAR: experiment switch for tools/kbench.hip (0 = production; 1 = no FFTs, memory only)
@@ -611,6 +642,17 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #ifndef GD_FUSED_GROUP
 #define GD_FUSED_GROUP 4
 #endif
+#ifndef GD_FUSED_STAGGER
+#define GD_FUSED_STAGGER 0  // experiment: first-wave workgroups on odd CU groups start this many 10-ns ticks late
+#endif
+__device__ __forceinline__ void fused_stagger() {
+#if GD_FUSED_STAGGER
+    if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < GD_FUSED_STAGGER) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
+}
 // A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
 // (and kept live from) an earlier phase's identical computation (register budget: 128 VGPRs at
 // 1024 threads).
@@ -660,10 +702,24 @@ __device__ __forceinline__ void fused_gather(const float2* S, int c, int j, floa
     }
 }
 
-// Spectral update of column kx (rows ky = j + F1 s of this lane).
-template <int L, bool FIRST, bool LAST>
+// Spectral update of column kx (rows ky = j + F1 s of this lane).  The first NPRE bins' state may
+// have been loaded ahead (fused_prefetch, issued before the column's gather and forward FFT so their
+// latency hides under that work); the rest is loaded here in groups of GD_FUSED_GROUP.
+#ifndef GD_FUSED_PRE
+#define GD_FUSED_PRE 0
+#endif
+template <int L, bool FIRST, bool LAST, int NPRE = GD_FUSED_PRE>
+__device__ __forceinline__ void fused_prefetch(const Args& a, GState (&pre)[NPRE > 0 ? NPRE : 1], int g, int kx,
+                                               int j) {
+    using FG = FusedGeo<L>;
+    const size_t ob = ((size_t)g * FG::K + opaque(kx)) * L + opaque(j);
+#pragma unroll
+    for (int s = 0; s < NPRE; ++s) pre[s] = gauss_load<FIRST, LAST>(a, ob + FG::F1 * s);
+    __builtin_amdgcn_sched_barrier(0);  // issue them here
+}
+template <int L, bool FIRST, bool LAST, int NPRE = GD_FUSED_PRE>
 __device__ __forceinline__ void fused_update(const Args& a, float2 (&C)[FusedGeo<L>::F2], int g, int kx, int j,
-                                             float r1, float r2, float r2n) {
+                                             float r1, float r2, float r2n, const GState (&pre)[NPRE > 0 ? NPRE : 1]) {
     using FG = FusedGeo<L>;
     constexpr float inv_n = float(1.0 / double(L * L));
     j = opaque(j);
@@ -674,8 +730,13 @@ __device__ __forceinline__ void fused_update(const Args& a, float2 (&C)[FusedGeo
     const size_t ob = ((size_t)g * FG::K + kx) * L;
 #pragma unroll
     for (int s = 0; s < FG::F2; ++s) {
-        C[s] = gauss_iter_elem<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
-        if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
+        if (s < NPRE)
+            C[s] = gauss_iter_st<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], pre[s < NPRE ? s : 0], r1, r2, r2n, true,
+                                              inv_n);
+        else
+            C[s] = gauss_iter_elem<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
+        if (s >= NPRE && (s - NPRE) % GD_FUSED_GROUP == GD_FUSED_GROUP - 1)
+            __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
     }
 }
 
@@ -704,6 +765,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     fill_twiddles<L>(tw, tid, FG::THREADS);
     const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
     GD_TRACE(0);
+    fused_stagger();
 
     // R: pair p = line + LINES q
     float2 X[FG::PPL][F2];
@@ -755,6 +817,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     }
     lds_barrier();
     GD_TRACE(3);
+    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);  // column A's first bins: in flight under gather + FFT
     // Columns 0 and L/2 are real sequences over the rows (Re / Im of the pairs' X_p[0], X_p[L/2]):
     // line 0 carries both as one complex column Z = c_0 + i c_{L/2}, splits the spectra after the
     // forward FFT (C_0 = (Z + conj Z(-ky))/2, C_{L/2} = (Z - conj Z(-ky))/2i), updates column 0 itself
@@ -789,7 +853,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
         nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
                                                  true, inv_n);
-    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n);
+    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
     lds_barrier();  // Nyquist results
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
@@ -825,12 +889,13 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     }
     lds_barrier();
     GD_TRACE(6);
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
     float2 Cb[F2];
     fused_gather<L>(S, line, j, Cb);
     lds_barrier();
     GD_TRACE(7);
     line_fft<L, false, true>(Cb, opaque(j), my, tw);
-    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n);
+    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
     line_fft<L, true, true>(Cb, opaque(j), my, tw);
 
     // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
@@ -962,6 +1027,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     }
     __builtin_amdgcn_sched_barrier(0);  // X dies here: keep its LDS stores ahead of column A's FFT
     GD_TRACE(4);
+    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);
 
     // column A in registers (S is occupied by slice B); columns 0 and L/2 ride together in line 0
     line_fft<L, false, true, true>(C, opaque(j), nullptr, tw);
@@ -981,7 +1048,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
         nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
                                                  true, inv_n);
-    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n);
+    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
     lds_barrier();  // Nyquist results
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
@@ -996,6 +1063,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     GD_TRACE(5);
 
     // B: gather, then column A's first-half rows -> S (row layout [yl][SLD], A at [line])
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
     float2 Cb[F2];
     fused_gather<L>(S, line, j, Cb);
     lds_barrier();  // slice B read -> row half spectra
@@ -1007,7 +1075,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     }
     __builtin_amdgcn_sched_barrier(0);  // C's first half dies here
     line_fft<L, false, true, true>(Cb, opaque(j), nullptr, tw);
-    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n);
+    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
     line_fft<L, true, true, true>(Cb, opaque(j), nullptr, tw);
     GD_TRACE(7);
 
