@@ -118,6 +118,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--e2e-sample", type=int, default=64, help="galaxies for the ResUNet end-to-end sample")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="skip the hipGraph-replay measurement")
     p.add_argument("--chunk-mb", type=float, default=None,
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
@@ -233,6 +234,28 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
+    # the same forward captured once as a hipGraph (gdeconv.graphs) and replayed: what a serving loop
+    # pays once host launch overhead is gone (matters at 48^2; reported beside value, not as value)
+    graphed = None
+    if not args.no_graph:
+        from gdeconv.graphs import GraphedForward
+        gf = GraphedForward(model, obs, psf, alpha)
+        gout = gf.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tg0 = time.perf_counter()
+        for _ in range(args.steps):
+            gout = gf.replay()
+        torch.cuda.synchronize()
+        tgr = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tgr, op=dist.ReduceOp.MAX)
+        tgr = float(tgr.item())
+        graphed = {"value": N * world * args.steps / tgr, "unit": "galaxies/s", "ms_per_step": tgr * 1e3 / args.steps,
+                   "bit_identical_to_eager": bool(torch.equal(gout, out))}
+        del gf, gout
+
     # live timing: HIP events recorded by the library on each kernel's launch stream and, for whole
     # operations (op_*), on the caller's stream, over the timed region
     kernels = {pretty(k): {"avg_ms": ms / c, "launches": c} for k, (ms, c) in kstats.items()}
@@ -290,6 +313,8 @@ def main():
     }
     if gather_ms is not None:
         rec["gather_ms"] = gather_ms
+    if graphed is not None:
+        rec["graphed"] = graphed
 
     if rank == 0 and world == 1 and not args.no_e2e:
         model.Z = denoiser

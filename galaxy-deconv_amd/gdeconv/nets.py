@@ -62,8 +62,20 @@ class ResUNet(nn.Module):
         self.m_up2 = _up(nc[2], nc[1], nb)
         self.m_up1 = _up(nc[1], nc[0], nb)
         self.m_tail = nn.Conv2d(nc[0], out_nc, 3, 1, 1, bias=False)
+        # NHWC activations on the GPU: MIOpen's fp32 NHWC convolutions run the denoiser ~11 % faster
+        # than NCHW on MI355X (tools/e2e_sweep.py: 89.8 -> 99.7 gal/s end to end at 256^2); same
+        # arithmetic type (fp32), no TF32.  The parameters keep their values (state_dict unchanged).
+        self.channels_last = True
 
     def forward(self, x):
+        if self.channels_last and x.is_cuda:
+            if not self.m_body[0].res[0].weight.is_contiguous(memory_format=torch.channels_last):
+                self.to(memory_format=torch.channels_last)
+            x = x.contiguous(memory_format=torch.channels_last)
+            return self._forward(x).contiguous()
+        return self._forward(x)
+
+    def _forward(self, x):
         h, w = x.shape[-2:]
         pb, pr = (-h) % 8, (-w) % 8
         if pb or pr:

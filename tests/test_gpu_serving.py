@@ -1,0 +1,91 @@
+"""GPU tests for the serving-side rows of SURVEY 8(f) rank 2 (end-to-end denoiser throughput):
+hipGraph capture of the whole unrolled forward (gdeconv.graphs) and the NHWC (channels_last)
+ResUNet.  Bars: a replayed graph runs the same kernels as the eager forward, so its output is
+bit-identical; the NHWC denoiser is fp32 like the NCHW one, so the full model stays within the
+1e-5 normwise parity bar of the golden vectors (tests/golden/admm48.npz)."""
+import numpy as np
+import pytest
+import torch
+
+import admm_oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+WEIGHT_SEED = 1234
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def nerr(out, ref):
+    return float(O.normwise_error(out, ref).max())
+
+
+def _model(n, llh, dev, identity=False):
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.weights import make_state_dict
+    m = Unrolled_ADMM(n_iters=n, llh=llh)
+    m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    m = m.to(dev).eval()
+    if identity:
+        m.Z = torch.nn.Identity()
+    return m
+
+
+@pytest.mark.parametrize("L,N", [(48, 37), (256, 5)])
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+def test_graphed_forward_engine_bit_identical(dev, L, N, llh):
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.synth import make_batch
+    m = _model(8, llh, dev, identity=True)
+    obs, psf, alpha, _ = make_batch(N, L, seed=9, device=dev)
+    with torch.no_grad():
+        eager = m(obs, psf, alpha)
+    g = GraphedForward(m, obs, psf, alpha, clone=True)
+    assert torch.equal(g(obs, psf, alpha), eager)
+    # new inputs through the same graph
+    obs2, psf2, alpha2, _ = make_batch(N, L, seed=10, device=dev)
+    with torch.no_grad():
+        eager2 = m(obs2, psf2, alpha2)
+    assert torch.equal(g(obs2, psf2, alpha2), eager2)
+
+
+def test_graphed_forward_full_model(dev):
+    """Whole model incl. SubNet and the ResUNet denoiser, captured at 48^2."""
+    from gdeconv.graphs import GraphedForward
+    g0 = golden("admm48.npz")
+    obs, psf, alpha = T(g0["obs"]).to(dev), T(g0["psf"]).to(dev), T(g0["alpha"]).to(dev)
+    m = _model(2, "Gaussian", dev)
+    with torch.no_grad():
+        eager = m(obs, psf, alpha)
+    g = GraphedForward(m, obs, psf, alpha, clone=True)
+    out = g(obs, psf, alpha)
+    assert nerr(out.cpu(), eager.cpu()) < 1e-6
+    assert nerr(out.cpu(), T(g0["Gaussian_n2_out"])) < TOL
+
+
+def test_graphed_forward_rejects_shape_change(dev):
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.synth import make_batch
+    m = _model(2, "Gaussian", dev, identity=True)
+    obs, psf, alpha, _ = make_batch(4, 48, seed=1, device=dev)
+    g = GraphedForward(m, obs, psf, alpha)
+    with pytest.raises(ValueError):
+        g(obs[:2], psf[:2], alpha[:2])
+
+
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+def test_channels_last_denoiser_parity(dev, llh):
+    """NHWC ResUNet (the GPU default) against the NCHW one and the reference golden output."""
+    g0 = golden("admm48.npz")
+    obs, psf, alpha = T(g0["obs"]).to(dev), T(g0["psf"]).to(dev), T(g0["alpha"]).to(dev)
+    m = _model(2, llh, dev)
+    with torch.no_grad():
+        out_cl = m(obs, psf, alpha).cpu()
+        m.Z.net.channels_last = False
+        m.Z.net.to(memory_format=torch.contiguous_format)
+        out_nchw = m(obs, psf, alpha).cpu()
+    assert nerr(out_cl, out_nchw) < 2e-6
+    assert nerr(out_cl, T(g0[f"{llh}_n2_out"])) < TOL
