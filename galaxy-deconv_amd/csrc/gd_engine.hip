@@ -1335,6 +1335,10 @@ inline int fail(int code, const char* msg) {
     g_last_error = msg;
     return code;
 }
+inline int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
 
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
@@ -1737,7 +1741,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.8"; }
+const char* gd_engine_rev(void) { return "r01.9"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2074,3 +2078,5 @@ int gd_subnet_features(const void* otf128_half, const float* params, float* feat
 }
 
 }  // extern "C"
+
+#include "gd_ingest.hpp"  // host-side packed-batch reader (C ABI gd_pack_*)

@@ -56,6 +56,11 @@ SIGNATURES = {
     "gd_profile_collect": (_I, []),
     "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),
     "gd_profile_reset": (_I, []),
+    "gd_pack_open": (_I, [ctypes.c_char_p, ctypes.POINTER(_P), ctypes.POINTER(_LL), ctypes.POINTER(_I)]),
+    "gd_pack_section_bytes": (_LL, [_P, _I]),
+    "gd_pack_read": (_I, [_P, _I, _LL, _LL, _P, _I]),
+    "gd_pack_gather": (_I, [_P, _I, _P, _LL, _P, _I]),
+    "gd_pack_close": (_I, [_P]),
 }
 
 _lib = None

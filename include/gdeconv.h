@@ -27,6 +27,9 @@
  *   gd_gx_init          models/unrolled_admm_gaussian.py:111-127  UnrolledADMMGaussian Y, H, init_l2
  *   gd_gx_xupdate       models/unrolled_admm_gaussian.py:85-93 (+ dual update :145, denoiser input :142)
  *   gd_gx_xupdate_backward  adjoint of XUpdateGaussian (autograd for train.py:41's model)
+ *   gd_pack_*           utils/utils_data.py:87-103 Galaxy_Dataset.__getitem__ (per-file torch.load of
+ *                       psf/obs/gt + alpha = obs.mean()) and :131-136 get_dataloader's batching: whole
+ *                       batches read from one packed file (host side; no device pointers)
  */
 #ifndef GDECONV_H
 #define GDECONV_H
@@ -174,6 +177,25 @@ int gd_profile_enable(int level);
 int gd_profile_collect(void);
 int gd_profile_get(int i, char* name, int name_len, double* total_ms, long long* launches);
 int gd_profile_reset(void);
+
+/* Packed galaxy datasets (GDPACK01; writer: gdeconv/ingest.py).  HOST-side entry points: `dst` is
+ * host memory (pinned by the caller for fast H2D), nothing touches the GPU.  Sections: */
+#define GD_PACK_OBS 0   /* fp32 [n][H][W] observations                         */
+#define GD_PACK_PSF 1   /* fp32 [n][h][w] PSFs                                 */
+#define GD_PACK_GT 2    /* fp32 [n][H][W] ground truth (when dims[4] != 0)     */
+#define GD_PACK_ALPHA 3 /* fp32 [n]       alpha = obs.ravel().mean() per galaxy */
+#define GD_PACK_INFO 4  /* UTF-8 JSON     the dataset's info.json (n_train, n_test, sequence, ...) */
+
+/* Open `path`; *n = galaxies, dims = {H, W, h, w, has_gt}.  *handle is freed by gd_pack_close. */
+int gd_pack_open(const char* path, void** handle, long long* n, int* dims);
+/* Bytes of a section (-1 on a bad handle / section). */
+long long gd_pack_section_bytes(void* handle, int section);
+/* Galaxies [g0, g0 + count) of a section -> dst (contiguous), read by up to nthreads pread threads.
+ * GD_PACK_INFO ignores g0 / count and copies the whole JSON (gd_pack_section_bytes bytes). */
+int gd_pack_read(void* handle, int section, long long g0, long long count, void* dst, int nthreads);
+/* Galaxies idx[0..count) of a section (0..3) -> dst in that order (shuffled batches). */
+int gd_pack_gather(void* handle, int section, const long long* idx, long long count, void* dst, int nthreads);
+int gd_pack_close(void* handle);
 
 #ifdef __cplusplus
 }
