@@ -29,10 +29,13 @@ MODE_NAMES = {
 def pretty(kname):
     if "k_subnet_features" in kname:
         return "k_subnet_features<128,FEATURES>"
-    m = re.search(r"k_gal_iter<(\d+), (true|false), (true|false)>", kname)
+    m = re.search(r"(k_gal_iter2?)<(\d+), (true|false), (true|false)>", kname)
     if m:
-        first, last = m.group(2) == "true", m.group(3) == "true"
-        return f"k_gal_iter<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
+        first, last = m.group(3) == "true", m.group(4) == "true"
+        return f"{m.group(1)}<{m.group(2)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
+    m = re.search(r"k_psf_rows<(\d+)>", kname)
+    if m:
+        return f"k_psf_rows<{m.group(1)},ROWS>"
     m = re.search(r"(k_\w+)<(\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
         return None
