@@ -1,1 +1,1 @@
-"""Reference-path shims (``utils.utils_torch``)."""
+"""Reference-path shims (``utils.utils_torch``, ``utils.utils_data``)."""

@@ -20,7 +20,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference"
 sys.path.insert(0, REF)
-from utils.utils_data import Galaxy_Dataset  # noqa: E402  (reference)
+from utils.utils_data import Galaxy_Dataset, down_sample, get_flux  # noqa: E402  (reference)
 
 N_TRAIN, N_TEST, H, h = 5, 3, 48, 48
 
@@ -61,6 +61,12 @@ def main():
             g[f"{tag}_psf"] = np.stack([it[0][1].numpy() for it in items])
             g[f"{tag}_alpha"] = np.stack([it[0][2].numpy() for it in items])
             g[f"{tag}_gt"] = np.stack([it[1].numpy() for it in items])
+    # the module's two helpers (generate_data.py uses them): 4x box down-sampling, magnitude -> flux
+    ds_in = np.random.default_rng(7).uniform(0, 1, (192, 192)).astype(np.float32)
+    g["ds_in"], g["ds_out"] = ds_in, down_sample(torch.from_numpy(ds_in)).numpy()
+    mags = np.array([20.0, 23.5, 25.2], np.float64)
+    g["flux_mag"] = mags
+    g["flux"] = np.array([get_flux(m, 30.0, 32.363, 4.5, 0.9) for m in mags], np.float64)
     np.savez_compressed(os.path.join(HERE, "ingest.npz"), **g)
     print({k: v.shape for k, v in g.items()})
 

@@ -142,3 +142,10 @@ def test_reader_errors(packed, tmp_path):
             pk.read("gt", 0, 1)
         with pytest.raises(EngineError, match="out of bounds"):
             pk.gather("obs", [0, 8])
+
+
+def test_utils_data_helpers_match_reference():
+    from utils.utils_data import down_sample, get_flux
+    assert np.array_equal(down_sample(torch.from_numpy(G["ds_in"])).numpy(), G["ds_out"])
+    got = np.array([get_flux(m, 30.0, 32.363, 4.5, 0.9) for m in G["flux_mag"]])
+    assert np.array_equal(got, G["flux"])
