@@ -43,6 +43,8 @@ MODE_NAMES = {
 def pretty(name):
     k, rest = name.split("<")
     L, mode = rest.rstrip(">").split(",")
+    if k == "op_rl":
+        return f"op_richardson_lucy<{L}>"
     if k.startswith("op_"):
         return f"{k}<{L},{['Gaussian', 'Poisson'][int(mode)]}>"
     return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
@@ -54,6 +56,8 @@ def op_bytes(name, L, n_iters, fused=False):
     z + state (|H|^2, G, U1, W~) in, U1, W~ + zin out = 2 img + 5.5 half (first: no U1 read; last: no
     G read, no state written); three-kernel: RF(z) + C_G_ITER + RI(zin) adds the workspace round trips."""
     img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
+    if pretty(name) == f"op_richardson_lucy<{L}>":
+        return survey_rl_bytes_per_galaxy(L, n_iters)
     if pretty(name) == f"op_admm_iter<{L},Gaussian>":
         if n == 1:
             c = 1.5 if fused else 5.5
@@ -105,6 +109,24 @@ def survey_bytes_per_galaxy(L, n, h=48):
     return 4 * L * L * (4 + 16 * n) + 4 * h * h
 
 
+def survey_rl_bytes_per_galaxy(L, n, h=48):
+    """Richardson-Lucy B = 4*HW*(3 + 4 n) + 4 h w per galaxy (per iteration: read x, y,
+    the OTF, write x)."""
+    return 4 * L * L * (3 + 4 * n) + 4 * h * h
+
+
+class RLForward(torch.nn.Module):
+    """``Richard_Lucy(n_iters).forward(y, psf)`` behind the (y, psf, alpha) call of the ADMM bench."""
+
+    def __init__(self, n_iters):
+        super().__init__()
+        from gdeconv.models import Richard_Lucy
+        self.rl = Richard_Lucy(n_iters)
+
+    def forward(self, y, psf, alpha=None):
+        return self.rl(y, psf)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -112,7 +134,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=4096, help="galaxies per GPU")
     p.add_argument("--size", type=int, default=256)
-    p.add_argument("--n-iters", type=int, default=8)
+    p.add_argument("--n-iters", type=int, default=None, help="default 8 (admm) / 100 (rl)")
+    p.add_argument("--workload", choices=["admm", "rl"], default="admm",
+                   help="admm: Unrolled_ADMM (BASELINE metric, configs[2]); rl: Richard_Lucy (configs[4])")
     p.add_argument("--llh", default="Gaussian")
     p.add_argument("--cpu-sample", type=int, default=64, help="galaxies in the CPU baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -147,6 +171,17 @@ def cpu_baseline(args):
     from gdeconv.synth import make_batch
     n = args.cpu_sample
     obs, psf, alpha, _ = make_batch(n, args.size, seed=777)
+    if args.workload == "rl":
+        O.richardson_lucy(obs[:1], psf[:1], 2)  # warm
+        t_total, done = 0.0, 0
+        while t_total < args.cpu_seconds or done == 0:
+            t0 = time.perf_counter()
+            O.richardson_lucy(obs, psf, args.n_iters)
+            t_total += time.perf_counter() - t0
+            done += n
+        return {"value": done / t_total, "unit": "galaxies/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"oracle/admm_oracle.richardson_lucy (PyTorch CPU restatement of the reference), "
+                          f"{n} galaxies x {args.size}^2, n_iters={args.n_iters}, {done // n} passes, {t_total:.1f}s"}
     m = build_model(args.n_iters, args.llh, "cpu")
     with torch.no_grad():
         rho1, rho2 = m.init(psf, alpha)
@@ -191,11 +226,20 @@ def main():
         lib.gd_set_pipeline_streams(args.pipe_streams)
     pipe_streams = lib.gd_set_pipeline_streams(0)
 
+    rl = args.workload == "rl"
+    if args.n_iters is None:
+        args.n_iters = 100 if rl else 8
+    if rl and args.cpu_sample == 64:
+        args.cpu_sample = 4                  # RL(100) on the CPU: ~1 s per 256^2 galaxy
     N, L, n = args.batch, args.size, args.n_iters
     obs, psf, alpha, _ = make_batch(N, L, seed=20250307 + rank, device=dev)
-    model = build_model(n, args.llh, dev)
-    denoiser = model.Z
-    model.Z = torch.nn.Identity()            # spectral engine: the HIP hot path
+    if rl:
+        model, denoiser = RLForward(n).to(dev), None
+        use_fused = False
+    else:
+        model = build_model(n, args.llh, dev)
+        denoiser = model.Z
+        model.Z = torch.nn.Identity()        # spectral engine: the HIP hot path
 
     def step():
         return model(obs, psf, alpha)
@@ -330,25 +374,34 @@ def main():
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic, "algorithmic_bytes_per_launch": per_gal * N if per_gal else None,
                 "avg_launch_ms": dom_ms}
-    engine_gbs = survey_bytes_per_galaxy(L, n) * gal_s / world / 1e9
+    survey_b = survey_rl_bytes_per_galaxy(L, n) if rl else survey_bytes_per_galaxy(L, n)
+    engine_gbs = survey_b * gal_s / world / 1e9
+    if rl:
+        metric = f"galaxies/sec ({L}x{L}, Richard_Lucy n_iters={n})"
+        workload = (f"Richard_Lucy(n_iters={n}) forward (OTF + {n} multiplicative FFT-conv iterations), "
+                    f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[4])")
+    else:
+        metric = f"galaxies/sec ({L}x{L}, n_iters={n}) - unrolled ADMM spectral engine"
+        workload = (f"Unrolled_ADMM(n_iters={n}, llh='{args.llh}') forward, denoiser=identity "
+                    f"(spectral engine: SubNet + OTF + init_l2 + {n} ADMM iterations), "
+                    f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])")
 
     rec = {
-        "metric": f"galaxies/sec ({L}x{L}, n_iters={n}) - unrolled ADMM spectral engine",
+        "metric": metric,
         "value": gal_s, "unit": "galaxies/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (gdeconv.synth, seeded); deterministic random weights (gdeconv.weights)",
-        "config": {"workload": f"Unrolled_ADMM(n_iters={n}, llh='{args.llh}') forward, denoiser=identity "
-                               f"(spectral engine: SubNet + OTF + init_l2 + {n} ADMM iterations), "
-                               f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])",
+        "config": {"workload": workload,
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
-                   "llh": args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
+                   "llh": None if rl else args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": ({1: "fused (k_gal_iter, one workgroup per galaxy)",
                                   2: "fused (k_gal_iter2, register transpose, one workgroup per galaxy)"}[fused]
-                                 if use_fused else "three-kernel")},
+                                 if use_fused else ("whole RL loop per Infinity-Cache chunk (RIF/C chain)" if rl
+                                                    else "three-kernel"))},
         "roofline": roofline,
-        "engine_hbm": {"survey_bytes_per_galaxy": survey_bytes_per_galaxy(L, n), "achieved_GBs_per_gpu": engine_gbs,
+        "engine_hbm": {"survey_bytes_per_galaxy": survey_b, "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},
         "kernels": kernels,
     }
@@ -359,7 +412,7 @@ def main():
     if ingest is not None:
         rec["ingest"] = ingest
 
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and not args.no_e2e and not rl:
         model.Z = denoiser
         G = min(args.e2e_sample, N)
         o2, p2, a2 = obs[:G].contiguous(), psf[:G].contiguous(), alpha[:G].contiguous()

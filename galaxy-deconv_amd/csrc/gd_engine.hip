@@ -642,17 +642,6 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #ifndef GD_FUSED_GROUP
 #define GD_FUSED_GROUP 4
 #endif
-#ifndef GD_FUSED_STAGGER
-#define GD_FUSED_STAGGER 0  // experiment: first-wave workgroups on odd CU groups start this many 10-ns ticks late
-#endif
-__device__ __forceinline__ void fused_stagger() {
-#if GD_FUSED_STAGGER
-    if (blockIdx.x < 256 && ((blockIdx.x >> 3) & 1)) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < GD_FUSED_STAGGER) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
-}
 // A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
 // (and kept live from) an earlier phase's identical computation (register budget: 128 VGPRs at
 // 1024 threads).
@@ -765,7 +754,6 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     fill_twiddles<L>(tw, tid, FG::THREADS);
     const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
     GD_TRACE(0);
-    fused_stagger();
 
     // R: pair p = line + LINES q
     float2 X[FG::PPL][F2];
@@ -1900,6 +1888,7 @@ int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, 
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.otf = reinterpret_cast<float2*>(otf_half);
     a.o0 = x;
+    ProfScope ps("op_rl<" + std::to_string(H) + ",0>", (hipStream_t)stream, 1);
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
 }
 
