@@ -1114,6 +1114,93 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     });
 }
 
+// ---------------------------------------------------------------- fused small-image Gaussian iteration
+// L <= 128 (LSST stamps are 48^2): a galaxy's whole half spectrum fits in LDS (9.6 KiB at 48^2, 66.5 KiB
+// at 128^2), so one 256-thread workgroup per galaxy runs the whole iteration on chip - row FFTs of z,
+// column FFTs + the spectral update (gauss_iter_elem, same state layout as k_col<G_ITER*>), inverse
+// column FFTs, inverse row FFTs, zin stored - in ONE launch instead of RF -> C -> RI through the
+// workspace.  Moves z, the state and zin only (the 2 img + 5.5 half of k_gal_iter).  A line's row
+// buffer for the post-FFT split is its own exchange area (F1 (F2 + 1) >= L + 2 for every plan).
+template <int L, bool FIRST, bool LAST>
+__global__ __launch_bounds__(256) void k_gal_small(Args a) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1, LINES = 256 / F1, XCH = xch_elems<L>();
+    static_assert(XCH >= L + 2, "row buffer inside the exchange area");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 S[K * L];  // [kx][ky]
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, 256);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    __syncthreads();
+
+    // R: row pair p -> FFT -> the two rows' half spectra into S (transposed)
+    const float* z = a.a0 + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+        float2 v[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) v[s] = make_float2(z[(2 * p) * L + j + F1 * s], z[(2 * p + 1) * L + j + F1 * s]);
+        line_fft<L, false>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) my[j + F1 * s] = v[s];
+        wave_lds_sync();
+        for (int k = j; k < K; k += F1) {
+            const float2 C = my[k], D = my[k == 0 ? 0 : L - k];
+            S[k * L + 2 * p] = make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));
+            S[k * L + 2 * p + 1] = make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+        }
+        wave_lds_sync();  // the next line_fft rewrites the area
+    }
+    __syncthreads();  // all of z read (zin may alias z), S complete
+
+    // C: column kx -> FFT -> spectral update -> IFFT (back in place)
+    for (int kx = line; kx < K; kx += LINES) {
+        float2 v[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) v[s] = S[kx * L + j + F1 * s];
+        line_fft<L, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + j;
+#pragma unroll
+        for (int s = 0; s < F2; ++s) v[s] = gauss_iter_elem<FIRST, LAST>(a, ob + F1 * s, v[s], r1, r2, r2n, true, inv_n);
+        line_fft<L, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) S[kx * L + j + F1 * s] = v[s];
+    }
+    __syncthreads();
+
+    // I: Hermitian-extended packed pair spectrum -> inverse row FFT -> zin (x on the last iteration)
+    float* out = a.o0 + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+        float2 v[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int k = j + F1 * s;
+            const bool self = (k == 0) || (2 * k == L);  // self-conjugate bins: real parts only (irfft)
+            float2 be, bo;
+            if (2 * k <= L) {
+                be = S[k * L + 2 * p];
+                bo = S[k * L + 2 * p + 1];
+            } else {
+                be = cconj(S[(L - k) * L + 2 * p]);
+                bo = cconj(S[(L - k) * L + 2 * p + 1]);
+            }
+            if (self) {
+                be.y = 0.f;
+                bo.y = 0.f;
+            }
+            v[s] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+        line_fft<L, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            out[(2 * p) * L + j + F1 * s] = v[s].x;
+            out[(2 * p + 1) * L + j + F1 * s] = v[s].y;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- RI: row inverse + sink
 template <int MODE>
 struct RiTraits {
@@ -1318,6 +1405,7 @@ constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
 constexpr const char* kGalIterName = "k_gal_iter";
 constexpr const char* kGalIter2Name = "k_gal_iter2";
+constexpr const char* kGalSmallName = "k_gal_small";
 
 inline int fail(int code, const char* msg) {
     g_last_error = msg;
@@ -1431,6 +1519,16 @@ struct Launcher {
         ProfScope ps(nm(kGalIter2Name, FIRST + 2 * LAST), st);
         hipLaunchKernelGGL((k_gal_iter2<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_iter2");
+    }
+    template <bool FIRST, bool LAST>
+    static int gal_small_v(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalSmallName, FIRST + 2 * LAST), st);
+        hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
+        return check_launch("k_gal_small");
+    }
+    static int gal_small(const Args& a, hipStream_t st) {
+        if (a.first) return a.last ? gal_small_v<true, true>(a, st) : gal_small_v<true, false>(a, st);
+        return a.last ? gal_small_v<false, true>(a, st) : gal_small_v<false, false>(a, st);
     }
     static int gal_iter(const Args& a, hipStream_t st, int variant) {
         if (variant == 2) {
@@ -1607,6 +1705,9 @@ struct Ops {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
         if constexpr (has_fused<L>()) {
             if (g_fused) return Lc::gal_iter(a, st0, g_fused);  // one pass, no workspace
+        }
+        if constexpr (L <= 128) {
+            if (g_fused) return Lc::gal_small(a, st0);  // whole spectrum in LDS, one pass
         }
         return for_chunks(a, L, st0, [&](const Args& b, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_ONE>(b, st));

@@ -207,22 +207,41 @@ template <int R>
 __device__ __forceinline__ float dpp_row_ror(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + R, 0xF, 0xF, false));
 }
+#ifndef GD_DPP_INPLACE
+#define GD_DPP_INPLACE 1  // in-place cycle walks (2 spare VGPRs) instead of full 16-element copies
+#endif
 template <int SGN, int B = 0>
 __device__ __forceinline__ void lane_rotate16(float2 (&x)[16], int j) {  // x[k] <- x[(k + SGN j) mod 16]
     if constexpr (B < 4) {  // stage B: rotate by 2^B where bit B of j is set (compile-time indices)
         constexpr int d = 1 << B;
         const bool c = (j >> B) & 1;
+#if GD_DPP_INPLACE
+        // the rotation by d splits into d cycles of 16/d registers: walk each cycle in place, keeping
+        // only its first (overwritten) element aside
+        static_for<0, d>([&](auto sc) {
+            constexpr int s0 = decltype(sc)::value;
+            const float2 first = x[s0];
+            static_for<0, 16 / d>([&](auto ic) {
+                constexpr int k = (s0 + SGN * d * decltype(ic)::value + 64) & 15;
+                constexpr int src = (k + SGN * d + 64) & 15;
+                // values made opaque first: a select of two array elements would otherwise be folded
+                // into a load from a selected address, i.e. a dynamically indexed array in scratch
+                float2 pv = (src == s0) ? first : x[src], q = x[k];
+                asm volatile("" : "+v"(pv.x), "+v"(pv.y), "+v"(q.x), "+v"(q.y));
+                x[k] = c ? pv : q;
+            });
+        });
+#else
         float2 t[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            // values made opaque first: a select of two array elements would otherwise be folded into
-            // a load from a selected address, i.e. a dynamically indexed array in scratch memory
             float2 p = x[(k + SGN * d) & 15], q = x[k];
             asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(q.x), "+v"(q.y));
             t[k] = c ? p : q;
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = t[k];
+#endif
         lane_rotate16<SGN, B + 1>(x, j);
     }
 }
@@ -235,16 +254,35 @@ __device__ __forceinline__ void dpp_rounds(float2 (&z)[16], const float2 (&v)[16
         dpp_rounds<R + 1>(z, v);
     }
 }
+template <int R>
+__device__ __forceinline__ void dpp_rounds_inplace(float2 (&v)[16]) {  // v[R] <- row_ror:R of v[R]
+    if constexpr (R < 16) {
+        v[R] = make_float2(dpp_row_ror<R>(v[R].x), dpp_row_ror<R>(v[R].y));
+        dpp_rounds_inplace<R + 1>(v);
+    }
+}
 __device__ __forceinline__ void transpose16_dpp(float2 (&v)[16], int j) {
     // w[c] = v[(c + j) mod 16]: round r then moves, with ONE register index for all lanes, element
     // j of lane j -/+ r (row_ror direction GD_DPP_ROR_DIR = +1 / -1)
     lane_rotate16<1>(v, j);
+#if GD_DPP_INPLACE && GD_DPP_ROR_DIR > 0
+    // round r in place: v[r] now holds lane j - r's element; want v[n1] = (that of lane n1), i.e.
+    // index (j - n1) mod 16 -> a compile-time register renaming v[m] <- v[(16 - m) mod 16]
+    dpp_rounds_inplace<1>(v);
+#pragma unroll
+    for (int m = 1; m < 8; ++m) {
+        const float2 t = v[m];
+        v[m] = v[16 - m];
+        v[16 - m] = t;
+    }
+#else
     float2 z[16];
     z[0] = v[0];
     dpp_rounds<1>(z, v);
     // z[r] holds lane n1 = j -/+ r; want v[n1] = z[(+/-(j - n1)) mod 16]
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = z[GD_DPP_ROR_DIR > 0 ? (16 - m) & 15 : m];
+#endif
     lane_rotate16<-1>(v, j);
 }
 

@@ -166,6 +166,34 @@ def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
     assert nerr(out_f[idx], ref) < TOL
 
 
+@pytest.mark.parametrize("L", [32, 48, 64, 96, 128])
+@pytest.mark.parametrize("n", [1, 3])
+def test_small_fused_iteration_matches_three_kernel_path(dev, L, n):
+    """k_gal_small (whole half spectrum in LDS, L <= 128; first / middle / last variants) against the
+    three-kernel path and the oracle, per-galaxy rho, ragged batch."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 29
+    obs, psf, alpha, _ = make_batch(N, L, h=min(48, L), seed=70 + n + L, device=dev)
+    gen = torch.Generator().manual_seed(L + n)
+    rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
+    old = lib.gd_set_fused_iteration(1)
+    try:
+        with torch.no_grad():
+            out_f = m(obs, psf, alpha).cpu()
+            lib.gd_set_fused_iteration(0)
+            out_t = m(obs, psf, alpha).cpu()
+    finally:
+        lib.gd_set_fused_iteration(old)
+    assert nerr(out_f, out_t) < 2e-6
+    idx = [0, 13, 28]
+    ref = O.admm_forward(obs[idx].cpu(), psf[idx].cpu(), alpha[idx].cpu(), rho1[idx].cpu(), rho2[idx].cpu())
+    assert nerr(out_f[idx], ref) < TOL
+
+
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
 def test_admm48_replay_reference_denoiser(dev, llh):
     """Feed the reference's own per-iteration denoiser outputs z back in: checks every spectral
