@@ -434,14 +434,24 @@ __device__ __forceinline__ float2 gauss_iter_elem(const Args& a, size_t o, float
     return gauss_iter_st<FIRST, LAST>(a, o, Zk, gauss_load<FIRST, LAST>(a, o), r1, r2, r2n, valid, inv_n);
 }
 
+#ifndef GD_COL_LEAN
+#define GD_COL_LEAN 0  // measured: no effect on the chunked paths (bound by L2-fabric traffic, not occupancy)
+#endif
+#ifndef GD_COL_DPP
+#define GD_COL_DPP 0  // same (occupancy 4 -> 6-7, no change in time)
+#endif
 // VAR: experiment switch for tools/kbench.hip (0 = production; 1 = no FFTs, memory only)
 template <int L, int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) void k_col(Args a) {
     using G = Geo<L>;
     using TR = ColTraits<MODE>;
     constexpr int F1 = G::F1, F2 = G::F2, K = G::K;
+    // lean twiddles (12 registers instead of 30 per line) where two spectra are live at once
+    constexpr bool CLEAN = GD_COL_LEAN && F2 == 16;
+    // register (DPP) transposes for 16 x 16 lines: no LDS exchange areas, occupancy set by VGPRs
+    constexpr bool CDPP = GD_COL_DPP && F1 == 16 && F2 == 16;
     __shared__ float2 tw[L];
-    __shared__ float2 xch[G::COL_LDS];
+    __shared__ float2 xch[CDPP ? 1 : G::COL_LDS];
     const int tid = threadIdx.x;
     const int line = tid / F1, j = tid - line * F1;
     const int f = blockIdx.x * G::LPB + line;
@@ -449,7 +459,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     const int fc = valid ? f : 0;
     const int g = fc / K, kx = fc - g * K;
     fill_twiddles<L>(tw, tid, 256);
-    float2* my = xch + line * G::XCH;
+    float2* my = CDPP ? nullptr : xch + line * G::XCH;
 
     float2 P[F2], Q[F2];
     const size_t c0 = tidx(g, 0, kx, 0, K, L), c1 = tidx(g, 1, kx, 0, K, L);
@@ -460,8 +470,8 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     }
     __syncthreads();  // twiddles
     if constexpr (TR::FWD && VAR != 1) {
-        line_fft<L, false>(P, j, my, tw);
-        if constexpr (TR::IN2) line_fft<L, false>(Q, j, my, tw);
+        line_fft<L, false, CLEAN, CDPP>(P, j, my, tw);
+        if constexpr (TR::IN2) line_fft<L, false, CLEAN, CDPP>(Q, j, my, tw);
     }
     // C_G_INIT: the OTF column H(., kx) from the PSF's row spectra P[kx][i] (k_psf_rows, T slot 1):
     // padded row ky holds psf row i = (ky + h/2) mod L when i < h, zero otherwise; then the column FFT.
@@ -475,7 +485,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             if (i >= L) i -= L;
             Hc[s] = (i < h) ? Pr[i] : make_float2(0.f, 0.f);
         }
-        line_fft<L, false>(Hc, j, my, tw);
+        line_fft<L, false, CLEAN, CDPP>(Hc, j, my, tw);
     }
     constexpr float inv_n = float(1.0 / double(L * L));  // exact for L = 2^k
     const size_t ob = ((size_t)g * K + kx) * L;
@@ -603,8 +613,8 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         if (valid && j == 0) a.o2[(size_t)g * K + kx] = drho * inv_n;
     }
     if constexpr (TR::HAS_OUT && MODE != C_FWD && VAR != 1) {
-        line_fft<L, true>(P, j, my, tw);
-        if constexpr (TR::OUT2) line_fft<L, true>(Q, j, my, tw);
+        line_fft<L, true, CLEAN, CDPP>(P, j, my, tw);
+        if constexpr (TR::OUT2) line_fft<L, true, CLEAN, CDPP>(Q, j, my, tw);
     }
     if (valid) {
         if constexpr (MODE == C_FWD) {
@@ -641,6 +651,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #endif
 #ifndef GD_FUSED_GROUP
 #define GD_FUSED_GROUP 4
+#endif
+#ifndef GD_ITER2_PARKA
+#define GD_ITER2_PARKA 1  // k_gal_iter2: park column A's second half in global memory during column B
 #endif
 // A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
 // (and kept live from) an earlier phase's identical computation (register budget: 128 VGPRs at
@@ -1061,7 +1074,14 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
         float2* rr = S + (j + F1 * s) * SLD;
         rr[line] = make_float2(C[s].x, l0 ? 0.f : C[s].y);  // column 0: real part (irfft)
     }
-    __builtin_amdgcn_sched_barrier(0);  // C's first half dies here
+#if GD_ITER2_PARKA
+    // column A's second-half rows wait for phase I half 1 in this galaxy's output rows [L/2, L)
+    // (written only at the very end; z is fully loaded since phase R): 16 VGPRs fewer under column B
+    float2* parkA = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L + (size_t)(L / 2) * L);
+#pragma unroll
+    for (int s = F2 / 2; s < F2; ++s) parkA[(s - F2 / 2) * FG::THREADS + tid] = C[s];
+#endif
+    __builtin_amdgcn_sched_barrier(0);  // C's first half (and with GD_ITER2_PARKA all of C) dies here
     line_fft<L, false, true, true>(Cb, opaque(j), nullptr, tw);
     fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
     line_fft<L, true, true, true>(Cb, opaque(j), nullptr, tw);
@@ -1076,7 +1096,12 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
 #pragma unroll
             for (int s = F2 / 2; s < F2; ++s) {
                 float2* rr = S + (j + F1 * s - L / 2) * SLD;
-                rr[line] = make_float2(C[s].x, l0 ? 0.f : C[s].y);
+#if GD_ITER2_PARKA
+                const float2 c = parkA[(s - F2 / 2) * FG::THREADS + opaque(tid)];
+#else
+                const float2 c = C[s];
+#endif
+                rr[line] = make_float2(c.x, l0 ? 0.f : c.y);
             }
         }
 #pragma unroll
