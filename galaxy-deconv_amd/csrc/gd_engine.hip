@@ -26,8 +26,13 @@
 //   Richard_Lucy.forward models/Richard_Lucy.py:10-24   -> RF_PSF_YP, C_OTF_CONV, RIF_RL_RATIO,
 //                                                          C_CONVC, RIF_RL_UPDATE / RI_RL_FINAL, C_CONV
 //
-// ADMM state carried between iterations (all [N,1,L,L] fp32): u1, w = v - u2, zin (denoiser input)
-// plus y and the half-spectrum OTF.  u2 and v are never stored: u2_{n+1} = Hx_{n+1} - w_n and
+// Whole-galaxy kernels (one workgroup per galaxy, spectra on chip) for the Gaussian ADMM path:
+//   k_gal_iter / k_gal_iter2 (256^2, registers + LDS, slices of 64 columns), k_gal_small (iteration,
+//   L <= 128, half spectrum in LDS), k_gal_small_init (init, L <= 96).  The Gaussian state is spectral
+//   (|H|^2, G, U1, W~); the Poisson state below stays spatial.
+//
+// Poisson ADMM state carried between iterations (all [N,1,L,L] fp32): u1, w = v - u2, zin (denoiser
+// input) plus y and the half-spectrum OTF.  u2 and v are never stored: u2_{n+1} = Hx_{n+1} - w_n and
 // v_{n+1} - u2_{n+1} is all the next X-update needs (algebraically identical to :207-213).
 #include <hip/hip_runtime.h>
 
@@ -1139,6 +1144,47 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     });
 }
 
+// Small-image helpers (L <= 128, spectra in LDS as D[kx][ky]):
+// a line's forward-FFT result (packed rows r, r+1) -> the two rows' half spectra, via the line's own
+// exchange area (F1 (F2 + 1) >= L + 2 for every plan)
+template <int L>
+__device__ __forceinline__ void small_split(const float2 (&v)[Plan<L>::F2], int j, float2* my, float2* D, int r) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1;
+#pragma unroll
+    for (int s = 0; s < F2; ++s) my[j + F1 * s] = v[s];
+    wave_lds_sync();
+    for (int k = j; k < K; k += F1) {
+        const float2 C = my[k], Dm = my[k == 0 ? 0 : L - k];
+        D[k * L + r] = make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+        D[k * L + r + 1] = make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x));
+    }
+    wave_lds_sync();  // the next line_fft rewrites the area
+}
+// rows r, r+1's half spectra in D -> their packed line spectrum over kx in [0, L) (Hermitian
+// extension; the self-conjugate bins kx = 0, L/2 keep real parts only, as irfft does)
+template <int L>
+__device__ __forceinline__ void small_gather(const float2* D, int j, int r, float2 (&v)[Plan<L>::F2]) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2;
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int k = j + F1 * s;
+        const bool self = (k == 0) || (2 * k == L);
+        float2 be, bo;
+        if (2 * k <= L) {
+            be = D[k * L + r];
+            bo = D[k * L + r + 1];
+        } else {
+            be = cconj(D[(L - k) * L + r]);
+            bo = cconj(D[(L - k) * L + r + 1]);
+        }
+        if (self) {
+            be.y = 0.f;
+            bo.y = 0.f;
+        }
+        v[s] = make_float2(be.x - bo.y, be.y + bo.x);
+    }
+}
+
 // ---------------------------------------------------------------- fused small-image Gaussian iteration
 // L <= 128 (LSST stamps are 48^2): a galaxy's whole half spectrum fits in LDS (9.6 KiB at 48^2, 66.5 KiB
 // at 128^2), so one 256-thread workgroup per galaxy runs the whole iteration on chip - row FFTs of z,
@@ -1168,15 +1214,7 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
 #pragma unroll
         for (int s = 0; s < F2; ++s) v[s] = make_float2(z[(2 * p) * L + j + F1 * s], z[(2 * p + 1) * L + j + F1 * s]);
         line_fft<L, false>(v, j, my, tw);
-#pragma unroll
-        for (int s = 0; s < F2; ++s) my[j + F1 * s] = v[s];
-        wave_lds_sync();
-        for (int k = j; k < K; k += F1) {
-            const float2 C = my[k], D = my[k == 0 ? 0 : L - k];
-            S[k * L + 2 * p] = make_float2(0.5f * (C.x + D.x), 0.5f * (C.y - D.y));
-            S[k * L + 2 * p + 1] = make_float2(0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
-        }
-        wave_lds_sync();  // the next line_fft rewrites the area
+        small_split<L>(v, j, my, S, 2 * p);
     }
     __syncthreads();  // all of z read (zin may alias z), S complete
 
@@ -1199,29 +1237,114 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
     float* out = a.o0 + (size_t)g * L * L;
     for (int p = line; p < L / 2; p += LINES) {
         float2 v[F2];
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int k = j + F1 * s;
-            const bool self = (k == 0) || (2 * k == L);  // self-conjugate bins: real parts only (irfft)
-            float2 be, bo;
-            if (2 * k <= L) {
-                be = S[k * L + 2 * p];
-                bo = S[k * L + 2 * p + 1];
-            } else {
-                be = cconj(S[(L - k) * L + 2 * p]);
-                bo = cconj(S[(L - k) * L + 2 * p + 1]);
-            }
-            if (self) {
-                be.y = 0.f;
-                bo.y = 0.f;
-            }
-            v[s] = make_float2(be.x - bo.y, be.y + bo.x);
-        }
+        small_gather<L>(S, j, 2 * p, v);
         line_fft<L, true>(v, j, my, tw);
 #pragma unroll
         for (int s = 0; s < F2; ++s) {
             out[(2 * p) * L + j + F1 * s] = v[s].x;
             out[(2 * p + 1) * L + j + F1 * s] = v[s].y;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fused small-image Gaussian init
+// L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
+// G = conj(H) F(max(y,0)/alpha), and iteration 0's W~ = (rho2 |H|^2 X0 + G) / (1 + rho2) (the V step of
+// :207 with u2 = 0, premultiplied by conj(H): k_col<C_G_W1>) in one workgroup per galaxy.  The
+// observation's and the placed PSF's half spectra both fit in LDS (2 x 37.6 KiB at 96^2), so
+// y -> |H|^2, G, X0 -> x0 = clamp(., 0, 1) = zin -> F(x0) -> W~ is one launch instead of
+// RF_YA -> psf_rows -> G_INIT -> RIF_CLAMP -> G_W1 through the workspace; same arithmetic as that chain.
+template <int L>
+__global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1, LINES = 256 / F1, XCH = xch_elems<L>();
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 S[K * L];   // [kx][ky]: row spectra of max(y,0)/alpha -> X0 -> row spectra of x0
+    __shared__ float2 SH[K * L];  // [kx][ky]: row spectra of the placed PSF
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, 256);
+    const float al = a.alpha(g), r2 = a.rho2n(g);
+    __syncthreads();
+
+    // R: pairs q < L/2 of max(y,0)/alpha, pairs q >= L/2 of the placed PSF -> row half spectra
+    const float* y = a.y + (size_t)g * L * L;
+    for (int q = line; q < L; q += LINES) {
+        const bool isp = q >= L / 2;
+        const int p = isp ? q - L / 2 : q;
+        float2 v[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int c = j + F1 * s;
+            v[s] = isp ? make_float2(shifted_psf(a, g, 2 * p, c, L), shifted_psf(a, g, 2 * p + 1, c, L))
+                       : make_float2(fmaxf(y[(2 * p) * L + c], 0.f) / al, fmaxf(y[(2 * p + 1) * L + c], 0.f) / al);
+        }
+        line_fft<L, false>(v, j, my, tw);
+        small_split<L>(v, j, my, isp ? SH : S, 2 * p);
+    }
+    __syncthreads();
+
+    // C1: columns of Y and H -> |H|^2, G (state); X0 = G / (|H|^2 + 1/alpha) -> inverse column FFT
+    for (int kx = line; kx < K; kx += LINES) {
+        float2 v[F2], hc[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            v[s] = S[kx * L + j + F1 * s];
+            hc[s] = SH[kx * L + j + F1 * s];
+        }
+        line_fft<L, false>(v, j, my, tw);
+        line_fft<L, false>(hc, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + j;
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const float hh = hc[s].x * hc[s].x + hc[s].y * hc[s].y;
+            const float2 Gk = cmulc(v[s], hc[s]);
+            a.s_hh[ob + F1 * s] = hh;
+            a.s_g[ob + F1 * s] = Gk;
+            const float lhs = hh + 1.0f / al;
+            v[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+        }
+        line_fft<L, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) S[kx * L + j + F1 * s] = v[s];
+    }
+    __syncthreads();
+
+    // I: X0's rows -> inverse row FFT -> x0 = clamp(., 0, 1) -> zin; forward row FFT of x0 -> S
+    float* zin = a.o2 + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+        float2 v[F2];
+        small_gather<L>(S, j, 2 * p, v);
+        line_fft<L, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int c = j + F1 * s;
+            const float p0 = fminf(fmaxf(v[s].x, 0.f), 1.f), p1 = fminf(fmaxf(v[s].y, 0.f), 1.f);
+            zin[(2 * p) * L + c] = p0;
+            zin[(2 * p + 1) * L + c] = p1;
+            v[s] = make_float2(p0, p1);
+        }
+        line_fft<L, false>(v, j, my, tw);
+        small_split<L>(v, j, my, S, 2 * p);
+    }
+    __syncthreads();
+
+    // C2: F(x0) columns -> iteration 0's W~ (|H|^2 and G re-read: this thread wrote them in C1)
+    const float d0 = 1.0f + r2;
+    for (int kx = line; kx < K; kx += LINES) {
+        float2 v[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) v[s] = S[kx * L + j + F1 * s];
+        line_fft<L, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + j;
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const float hh = a.s_hh[ob + F1 * s];
+            const float2 Gk = a.s_g[ob + F1 * s];
+            a.s_w[ob + F1 * s] =
+                make_float2((r2 * (hh * v[s].x + 0.0f) + Gk.x) / d0, (r2 * (hh * v[s].y + 0.0f) + Gk.y) / d0);
         }
     }
 }
@@ -1431,6 +1554,7 @@ constexpr const char* kRowInvFwdName = "k_row_invfwd";
 constexpr const char* kGalIterName = "k_gal_iter";
 constexpr const char* kGalIter2Name = "k_gal_iter2";
 constexpr const char* kGalSmallName = "k_gal_small";
+constexpr const char* kGalSmallInitName = "k_gal_small_init";
 
 inline int fail(int code, const char* msg) {
     g_last_error = msg;
@@ -1550,6 +1674,11 @@ struct Launcher {
         ProfScope ps(nm(kGalSmallName, FIRST + 2 * LAST), st);
         hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
         return check_launch("k_gal_small");
+    }
+    static int gal_small_init(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalSmallInitName, 0), st);
+        hipLaunchKernelGGL((k_gal_small_init<L>), dim3(a.N), dim3(256), 0, st, a);
+        return check_launch("k_gal_small_init");
     }
     static int gal_small(const Args& a, hipStream_t st) {
         if (a.first) return a.last ? gal_small_v<true, true>(a, st) : gal_small_v<true, false>(a, st);
@@ -1715,6 +1844,9 @@ struct Ops {
     }
     static int admm_init_gauss(Args a0, hipStream_t st0) {
         // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
+        if constexpr (L <= 96) {
+            if (g_fused) return Lc::gal_small_init(a0, st0);  // both spectra in LDS, one pass
+        }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::template rf<RF_YA>(b, st));
@@ -1855,7 +1987,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.9"; }
+const char* gd_engine_rev(void) { return "r01.10"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 

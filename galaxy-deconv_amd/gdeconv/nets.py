@@ -100,9 +100,23 @@ class ZUpdateResUNet(nn.Module):
     def __init__(self, nc=(64, 128, 256, 512)):
         super().__init__()
         self.net = ResUNet(nc=tuple(nc))
+        # galaxies per denoiser call: the ResUNet's activations are ~80 MB per 256^2 galaxy, so the
+        # 4096-galaxy batch of configs[2] (~330 GB) must be micro-batched (hard parts).
+        # None = auto: 2^25 pixels per call (512 galaxies at 256^2, ~40 GB).
+        self.micro_batch = None
 
     def forward(self, z):
-        return self.net(z.float())
+        z = z.float()
+        N = z.shape[0]
+        mb = self.micro_batch or max(1, (1 << 25) // max(1, z.shape[-1] * z.shape[-2]))
+        if N <= mb:
+            return self.net(z)
+        if torch.is_grad_enabled():
+            return torch.cat([self.net(z[i:i + mb]) for i in range(0, N, mb)])
+        out = torch.empty_like(z)
+        for i in range(0, N, mb):
+            out[i:i + mb] = self.net(z[i:i + mb])
+        return out
 
 
 def _fold_conv_bn(conv, bn):

@@ -167,10 +167,10 @@ def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
 
 
 @pytest.mark.parametrize("L", [32, 48, 64, 96, 128])
-@pytest.mark.parametrize("n", [1, 3])
+@pytest.mark.parametrize("n", [0, 1, 3])
 def test_small_fused_iteration_matches_three_kernel_path(dev, L, n):
-    """k_gal_small (whole half spectrum in LDS, L <= 128; first / middle / last variants) against the
-    three-kernel path and the oracle, per-galaxy rho, ragged batch."""
+    """k_gal_small_init (L <= 96) + k_gal_small (whole half spectrum in LDS, L <= 128; first / middle /
+    last variants) against the chunked multi-kernel path and the oracle, per-galaxy rho, ragged batch."""
     from gdeconv import _lib
     from gdeconv.synth import make_batch
     lib = _lib.load()
@@ -188,10 +188,14 @@ def test_small_fused_iteration_matches_three_kernel_path(dev, L, n):
             out_t = m(obs, psf, alpha).cpu()
     finally:
         lib.gd_set_fused_iteration(old)
-    assert nerr(out_f, out_t) < 2e-6
-    idx = [0, 13, 28]
-    ref = O.admm_forward(obs[idx].cpu(), psf[idx].cpu(), alpha[idx].cpu(), rho1[idx].cpu(), rho2[idx].cpu())
-    assert nerr(out_f[idx], ref) < TOL
+    # two fp32 paths (different kernels, FMA contraction): a few ulp of x0's spectrum through the
+    # init's divide and clamp - both are held to the oracle bar below on every galaxy
+    e_ft = nerr(out_f, out_t)
+    ref = O.admm_forward(obs.cpu(), psf.cpu(), alpha.cpu(), rho1.cpu(), rho2.cpu())
+    e_f, e_t = nerr(out_f, ref), nerr(out_t, ref)
+    print(f"L={L} n={n}: fused vs chunked {e_ft:.2e}, vs oracle {e_f:.2e} / {e_t:.2e}")
+    assert e_ft < 5e-6
+    assert e_f < TOL and e_t < TOL
 
 
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
