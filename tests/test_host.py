@@ -103,3 +103,27 @@ def test_subnet_bn_folding_matches_reference_order():
         c1, _ = net(psf, alpha)          # cached folded weights reused
     assert torch.allclose(a1, b1, rtol=2e-5, atol=1e-7) and torch.allclose(a2, b2, rtol=2e-5, atol=1e-7)
     assert torch.equal(b1, c1)
+
+
+def test_denoiser_micro_batching_is_transparent():
+    """ZUpdateResUNet splits large batches into micro-batches (activations of a 4096 x 256^2 batch do
+    not fit in HBM); per-galaxy results equal the one-call results (CPU, fp32), with and without
+    autograd."""
+    from gdeconv.nets import ZUpdateResUNet
+    from gdeconv.weights import make_state_dict
+    torch.manual_seed(0)
+    z = ZUpdateResUNet(nc=(8, 16, 32, 64))
+    z.load_state_dict(make_state_dict(z, 7))
+    z.eval()
+    x = torch.rand(5, 1, 24, 24)
+    with torch.no_grad():
+        full = z(x)
+        z.micro_batch = 2
+        part = z(x)
+    assert torch.allclose(part, full, rtol=0, atol=1e-6 * float(full.abs().max()))
+    xg = x.clone().requires_grad_(True)
+    z(xg).sum().backward()
+    z.micro_batch = None
+    xf = x.clone().requires_grad_(True)
+    z(xf).sum().backward()
+    assert torch.allclose(xg.grad, xf.grad, rtol=0, atol=1e-6 * float(xf.grad.abs().max()))
