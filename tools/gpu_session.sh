@@ -15,5 +15,11 @@ run trace && (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $
 run pmc_fetch && (cd /tmp && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_col|k_row|k_gal|k_psf|k_subnet" -d $O/prof_fetch -o fetch --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-graph --no-ingest > /dev/null 2> $O/pmc_fetch.err) &&
 run pmc_write && (cd /tmp && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_col|k_row|k_gal|k_psf|k_subnet" -d $O/prof_write -o write --output-format csv -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-graph --no-ingest > /dev/null 2> $O/pmc_write.err)
 rc=$?
+[ $rc -eq 0 ] && run torchrun1 && timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $O/bench_torchrun1.json 2> $O/bench_torchrun1.err
+rc=$?
+[ $rc -eq 0 ] && run bench48 && timeout -k 10 300 python3 bench.py --size 48 --batch 256 --no-cpu-baseline > $O/bench48.json 2> $O/bench48.err
+rc=$?
+[ $rc -eq 0 ] && run bench_rl && timeout -k 10 300 python3 bench.py --workload rl > $O/bench_rl.json 2> $O/bench_rl.err
+rc=$?
 echo "[session] rc=$rc" >&2
 exit $rc
