@@ -27,8 +27,9 @@
 //                                                          C_CONVC, RIF_RL_UPDATE / RI_RL_FINAL, C_CONV
 //
 // Whole-galaxy kernels (one workgroup per galaxy, spectra on chip) for the Gaussian ADMM path:
-//   k_gal_iter / k_gal_iter2 (256^2, registers + LDS, slices of 64 columns), k_gal_small (iteration,
-//   L <= 128, half spectrum in LDS), k_gal_small_init (init, L <= 96).  The Gaussian state is spectral
+//   k_gal_iter / k_gal_iter2 (256^2, registers + LDS, slices of 64 columns), k_gal_iter<KM = 1> +
+//   k_gal_w1 (init at 256^2), k_gal_small (iteration, L <= 128, half spectrum in LDS),
+//   k_gal_small_init (init, L <= 96).  The Gaussian state is spectral
 //   (|H|^2, G, U1, W~); the Poisson state below stays spatial.
 //
 // Poisson ADMM state carried between iterations (all [N,1,L,L] fp32): u1, w = v - u2, zin (denoiser
@@ -323,7 +324,9 @@ __global__ __launch_bounds__((RowGeo<L, RfTraits<MODE>::NI, RBX>::THREADS)) void
 // padded column (jj - h/2) mod L.  Rows 2p, 2p+1 ride one complex line (same image: the packing
 // rule), split after the FFT and stored compactly as P[kx][i] (i < h, contiguous) in T slot 1, where
 // k_col<C_G_INIT> picks its OTF column up with a few coalesced loads.
-template <int L>
+// TO_STATE: write the compact rows into this galaxy's U1 state slot instead (the fused init reads them
+// there; U1 is first written by iteration 0, which does not read it), [kx][i] at s_u1 + g K L.
+template <int L, bool TO_STATE = false>
 __global__ __launch_bounds__(256) void k_psf_rows(Args a) {
     using G = Geo<L>;
     constexpr int F1 = G::F1, F2 = G::F2, LPB = G::LPB, K = G::K;
@@ -350,15 +353,21 @@ __global__ __launch_bounds__(256) void k_psf_rows(Args a) {
 #pragma unroll
     for (int s = 0; s < F2; ++s) lds[line * G::RLD + j + F1 * s] = v[s];
     __syncthreads();
-    float2* P = a.T + tidx(g, 1, 0, 0, K, L);
+    float2* P = TO_STATE ? a.s_u1 + (size_t)g * K * L : a.T + tidx(g, 1, 0, 0, K, L);
     for (int idx = tid; idx < LPB * K; idx += 256) {
         const int m = idx % LPB, k = idx / LPB;
         if (p0 + m >= pairs) continue;
         const float2 C = lds[m * G::RLD + k];
         const float2 D = lds[m * G::RLD + (k == 0 ? 0 : L - k)];
         // row 2p: (C + conj D)/2 ; row 2p+1: (C - conj D)/(2i) -> adjacent: one 16-byte store
-        *reinterpret_cast<float4*>(P + (size_t)k * h + 2 * (p0 + m)) =
-            make_float4(0.5f * (C.x + D.x), 0.5f * (C.y - D.y), 0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+        float4 o = make_float4(0.5f * (C.x + D.x), 0.5f * (C.y - D.y), 0.5f * (C.y + D.y), 0.5f * (D.x - C.x));
+        if (TO_STATE && k == 0) {
+            // rows' bins 0 and L/2 are real (D = C there): kx = 0 holds P_0 + i P_{L/2}, the packed
+            // column the fused init's line 0 transforms (kx = L/2 is not read)
+            const float2 Cn = lds[m * G::RLD + L / 2];
+            o = make_float4(C.x, Cn.x, C.y, Cn.y);
+        }
+        *reinterpret_cast<float4*>(P + (size_t)k * h + 2 * (p0 + m)) = o;
     }
 }
 
@@ -755,7 +764,107 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int L, bool FIRST, bool LAST>
+// ---- the fused Gaussian init on the same skeleton (KM: 0 = iteration, 1 = init; iteration 0's W~ is
+// k_gal_w1 below)
+//   KM = 1  y -> max(y,0)/alpha -> R, A, B with the OTF column built in-kernel: |H|^2, G (state), X0 =
+//           G / (|H|^2 + 1/alpha) -> inverse -> I: x0 = clamp(., 0, 1) -> zin   (RF_YA, C_G_INIT, RIF_CLAMP)
+// The OTF column kx comes from the PSF's compact row spectra (k_psf_rows<L, true>, parked in the U1
+// slot): placed row ky holds psf row i = (ky + h/2) mod L when i < h.  Line 0 carries columns 0 and
+// L/2 (real over the rows) packed as P0 + i P_{L/2}, like the data, and splits them after the FFT.
+template <int L>
+__device__ __forceinline__ void init_hload(const Args& a, float2 (&Hc)[FusedGeo<L>::F2], int g, int kx, int j) {
+    using FG = FusedGeo<L>;
+    static_assert((L & (L - 1)) == 0, "power-of-two side");
+    const int h = a.h, c0p = h >> 1;
+    const float2* P0 = a.s_u1 + (size_t)g * FG::K * L + (size_t)opaque(kx) * h;  // kx = 0: P_0 + i P_{L/2}
+    j = opaque(j);
+    // h <= 64 (the host checks): rows ky in [2 F1, L - 2 F1) are zero for every lane, so only lane
+    // registers 0, 1, F2-2, F2-1 are loaded and the others are compile-time zeros (the first DFT
+    // stage folds them away)
+    static_assert(FG::F1 == 16 && FG::F2 == 16, "sparse OTF column for 16 x 16 lines");
+#pragma unroll
+    for (int s = 0; s < FG::F2; ++s) {
+        Hc[s] = make_float2(0.f, 0.f);
+        if (s < 2 || s >= FG::F2 - 2) {
+            const int i = (j + FG::F1 * s + c0p) & (L - 1);
+            if (i < h) Hc[s] = P0[i];
+        }
+    }
+}
+// The OTF column's FFT runs with register (DPP) transposes while the data column waits in the line's
+// LDS exchange area (register budget: the two columns are never both in registers).  Line 0 splits
+// the packed columns through nyqh (all reads before any write).
+template <int L>
+__device__ __forceinline__ void init_hfft(float2 (&Hc)[FusedGeo<L>::F2], int j, bool l0, const float2* tw,
+                                          float2* nyqh) {
+    using FG = FusedGeo<L>;
+    line_fft<L, false, true, true>(Hc, opaque(j), nullptr, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < FG::F2; ++s) nyqh[j + FG::F1 * s] = Hc[s];
+        wave_lds_sync();
+        float2 zm[FG::F2];
+#pragma unroll
+        for (int s = 0; s < FG::F2; ++s) zm[s] = nyqh[(L - j - FG::F1 * s) & (L - 1)];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < FG::F2; ++s) {
+            const float2 z = Hc[s];
+            nyqh[j + FG::F1 * s] = make_float2(0.5f * (z.y + zm[s].y), 0.5f * (zm[s].x - z.x));
+            Hc[s] = make_float2(0.5f * (z.x + zm[s].x), 0.5f * (z.y - zm[s].y));
+        }
+    }
+}
+template <int L>
+__device__ __forceinline__ void stash(float2* my, const float2 (&C)[FusedGeo<L>::F2], int j) {
+#pragma unroll
+    for (int s = 0; s < FusedGeo<L>::F2; ++s) my[j + FusedGeo<L>::F1 * s] = C[s];
+    wave_lds_sync();
+}
+template <int L>
+__device__ __forceinline__ void unstash(const float2* my, float2 (&C)[FusedGeo<L>::F2], int j) {
+    wave_lds_sync();
+#pragma unroll
+    for (int s = 0; s < FusedGeo<L>::F2; ++s) C[s] = my[j + FusedGeo<L>::F1 * s];
+}
+// init_l2 (models/Unrolled_ADMM.py:170-175) per bin: |H|^2, G = conj(H) F(max(y,0)/alpha) kept as
+// state; returns X0 / L^2 = G / (|H|^2 + 1/alpha) / L^2 (the arithmetic of k_col<C_G_INIT>)
+__device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, float2 Hk, float al, float inv_n) {
+    const float hh = Hk.x * Hk.x + Hk.y * Hk.y;
+    const float2 Gk = cmulc(Yk, Hk);
+    a.s_hh[o] = hh;
+    a.s_g[o] = Gk;
+    const float lhs = hh + 1.0f / al;
+    return cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+}
+// iteration 0's W~ (k_col<C_G_W1>'s arithmetic): the V step (:335-336) with Hx = H X0, u2 = 0, times conj(H)
+__device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk, float r2n) {
+    const float hh = a.s_hh[o];
+    const float2 Gk = a.s_g[o];
+    const float d0 = 1.0f + r2n;
+    a.s_w[o] = make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
+}
+template <int L, int KM>
+__device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<L>::F2],
+                                            const float2 (&Hc)[KM == 1 ? FusedGeo<L>::F2 : 1], int g, int kx, int j,
+                                            float al, float r2n) {
+    using FG = FusedGeo<L>;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    j = opaque(j);
+    kx = opaque(kx);
+    __builtin_amdgcn_sched_barrier(0);
+    const size_t ob = ((size_t)g * FG::K + kx) * L + j;
+#pragma unroll
+    for (int s = 0; s < FG::F2; ++s) {
+        if constexpr (KM == 1)
+            C[s] = init_bin(a, ob + FG::F1 * s, C[s], Hc[s], al, inv_n);
+        else
+            w1_bin(a, ob + FG::F1 * s, C[s], r2n);
+        if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int L, bool FIRST, bool LAST, int KM = 0>
 __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     using FG = FusedGeo<L>;
     constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, ALD = FG::ALD, LINES = FG::LINES;
@@ -765,23 +874,32 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
     __shared__ float nyqo[L];       // x(., L/2)
+    __shared__ float2 nyqh[KM == 1 ? L : 1];  // init: the OTF's Nyquist column
+    static_assert(KM == 0 || (KM == 1 && !FIRST && !LAST), "init variant");
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
     const bool l0 = (line == 0);
     float2* my = S + line * FG::XCH;
     fill_twiddles<L>(tw, tid, FG::THREADS);
-    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    const float r1 = KM == 0 ? a.rho1(g) : 0.f, r2 = KM == 0 ? a.rho2(g) : 0.f;
+    const float r2n = (LAST || KM != 0) ? 0.f : a.rho2n(g);
+    const float al = KM == 1 ? a.alpha(g) : 1.f;
     GD_TRACE(0);
 
-    // R: pair p = line + LINES q
+    // R: pair p = line + LINES q  (KM = 1: max(y,0)/alpha, RF_YA)
     float2 X[FG::PPL][F2];
     {
-        const float* z = a.a0 + (size_t)g * L * L;
+        const float* z = (KM == 0 ? a.a0 : a.y) + (size_t)g * L * L;
 #pragma unroll
         for (int q = 0; q < FG::PPL; ++q) {
             const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
 #pragma unroll
-            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+            for (int r = 0; r < F2; ++r) {
+                if constexpr (KM == 1)
+                    X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
+                else
+                    X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+            }
         }
     }
     __syncthreads();  // twiddles; all of z loaded (zin may alias z: the park stores below write it)
@@ -794,7 +912,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     // results.  Lane-contiguous (512 B per wave instruction),
     // read back by the same thread; every parked value is read back (and consumed into LDS) before
     // phase I writes that part of the image.
-    float2* park0 = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L);
+    // (KM = 1 parks in zin, its output)
+    float2* park0 = reinterpret_cast<float2*>((KM == 1 ? a.o2 : a.o0) + (size_t)g * L * L);
     float2* park1 = park0 + (size_t)L * L / 4;
     constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
     constexpr int NPB = GD_FUSED_NPB;                   // of which parked
@@ -831,6 +950,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     // and hands column L/2 to the first L/64 waves, one element per thread; the results are packed
     // back the same way, so the inverse FFT's real / imaginary parts are x(., 0) and x(., L/2) (only
     // real parts are kept for the self-conjugate row bins, as irfft does).
+    float2 Hc[KM == 1 ? F2 : 1];
     float2 C[F2];
     fused_gather<L>(S, line, j, C);
 #pragma unroll
@@ -855,11 +975,25 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
         }
         wave_lds_sync();  // (the inverse FFT rewrites the exchange area)
     }
-    lds_barrier();  // nyqc complete
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
-                                                 true, inv_n);
-    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
+    if constexpr (KM == 1) {
+        stash<L>(my, C, j);
+        init_hload<L>(a, Hc, g, line, j);
+        init_hfft<L>(Hc, j, l0, tw, nyqh);
+    }
+    lds_barrier();  // nyqc (nyqh) complete
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
+        const size_t on = ((size_t)g * FG::K + L / 2) * L + tid;
+        if constexpr (KM == 0)
+            nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
+        else
+            nyqc[tid] = init_bin(a, on, nyqc[tid], nyqh[tid], al, inv_n);
+    }
+    if constexpr (KM == 0) {
+        fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
+    } else {
+        unstash<L>(my, C, j);
+        init_update<L, KM>(a, C, Hc, g, line, j, al, r2n);
+    }
     lds_barrier();  // Nyquist results
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
@@ -901,12 +1035,20 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     lds_barrier();
     GD_TRACE(7);
     line_fft<L, false, true>(Cb, opaque(j), my, tw);
-    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
+    if constexpr (KM == 0) {
+        fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
+    } else {
+        stash<L>(my, Cb, j);
+        init_hload<L>(a, Hc, g, KS + line, j);
+        init_hfft<L>(Hc, j, false, tw, nyqh);
+        unstash<L>(my, Cb, j);
+        init_update<L, KM>(a, Cb, Hc, g, KS + line, j, al, r2n);
+    }
     line_fft<L, true, true>(Cb, opaque(j), my, tw);
 
     // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
     // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
-    float* out = a.o0 + (size_t)g * L * L;
+    float* out = (KM == 1 ? a.o2 : a.o0) + (size_t)g * L * L;
     static_for<0, 2>([&](auto hfc) {
         constexpr int hf = decltype(hfc)::value;
         lds_barrier();  // exchange areas -> row half spectra
@@ -943,11 +1085,118 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
         float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
 #pragma unroll
         for (int r = 0; r < F2; ++r) {
-            o[F1 * r] = V[r].x;
-            o[L + F1 * r] = V[r].y;
+            if constexpr (KM == 1) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
+                o[F1 * r] = fminf(fmaxf(V[r].x, 0.f), 1.f);
+                o[L + F1 * r] = fminf(fmaxf(V[r].y, 0.f), 1.f);
+            } else {
+                o[F1 * r] = V[r].x;
+                o[L + F1 * r] = V[r].y;
+            }
         }
         GD_TRACE(8 + hf);
     });
+}
+
+// Iteration 0's W~ for the fused init (C_G_W1's arithmetic: W~ = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2))
+// without parking: no inverse follows, so once column A is gathered into registers, slice B's bins
+// go straight from the row FFTs' registers into S, and column A is transformed with register (DPP)
+// transposes while S holds them.  Moves x0 = zin, |H|^2, G in and W~ out (3.5 words per pixel).
+template <int L>
+__global__ __launch_bounds__(1024) void k_gal_w1(Args a) {
+    using FG = FusedGeo<L>;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
+    static_assert(F1 == 16 && F2 == 16, "register transposes for 16 x 16 lines");
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
+    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // line 0's split scratch, then the Nyquist column's spectrum
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * FG::XCH;
+    fill_twiddles<L>(tw, tid, FG::THREADS);
+    const float r2n = a.rho2n(g);
+    float2 X[FG::PPL][F2];
+    {
+        const float* z = a.o2 + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+        }
+    }
+    __syncthreads();  // twiddles
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
+    lds_barrier();  // exchange areas -> slice A
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        const int p = line + LINES * q;
+        float2* row = S + p * SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = j + F1 * r;
+            if (r < KS / F1) row[k] = X[q][r];
+            if (r == 0 && j == 0) row[KS] = X[q][r];
+            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];
+            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];
+        }
+    }
+    lds_barrier();
+    float2 C[F2];
+    {  // fused_gather with few LDS loads in flight (slice B is still in registers)
+        const int c = opaque(line), jj = opaque(j);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int y = jj + F1 * s;
+            const float2 u = S[(y >> 1) * SLD + c], v = S[(y >> 1) * SLD + KS + c];
+            C[s] = (y & 1) ? make_float2(0.5f * (u.y + v.y), 0.5f * (v.x - u.x))
+                           : make_float2(0.5f * (u.x + v.x), 0.5f * (u.y - v.y));
+            const float2 w = nyq[y >> 1];
+            if (l0) C[s].y = (y & 1) ? w.y : w.x;
+            if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    lds_barrier();  // S -> slice B (k_gal_iter's phase-B layout)
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        float2* row = S + (line + LINES * q) * SLD;
+#pragma unroll
+        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
+            const int k = j + F1 * r;
+            if (r < 2 * KS / F1) row[k - KS] = X[q][r];
+            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
+                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // slice B leaves the registers before the transform
+    line_fft<L, false, true, true>(C, opaque(j), nullptr, tw);
+    if (l0) {  // columns 0 and L/2 out of the packed column (k_gal_iter's split, scratch nyqc)
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqc[j + F1 * s] = C[s];
+        wave_lds_sync();
+        float2 zm[F2];
+#pragma unroll
+        for (int s = 0; s < F2; ++s) zm[s] = nyqc[(L - j - F1 * s) & (L - 1)];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const float2 z = C[s];
+            nyqc[j + F1 * s] = make_float2(0.5f * (z.y + zm[s].y), 0.5f * (zm[s].x - z.x));
+            C[s] = make_float2(0.5f * (z.x + zm[s].x), 0.5f * (z.y - zm[s].y));
+        }
+    }
+    lds_barrier();  // nyqc and slice B complete
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
+        w1_bin(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r2n);
+    const float2 dummy[1] = {make_float2(0.f, 0.f)};
+    init_update<L, 2>(a, C, dummy, g, line, j, 1.f, r2n);
+    fused_gather<L>(S, line, j, C);
+    lds_barrier();  // S -> exchange areas
+    line_fft<L, false, true>(C, opaque(j), my, tw);
+    init_update<L, 2>(a, C, dummy, g, KS + line, j, 1.f, r2n);
 }
 
 // No-park variant (gd_set_fused_iteration(2)): the column transforms use the register (DPP) transpose,
@@ -1553,6 +1802,7 @@ constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
 constexpr const char* kGalIterName = "k_gal_iter";
 constexpr const char* kGalIter2Name = "k_gal_iter2";
+constexpr const char* kGalInitName = "k_gal_init";
 constexpr const char* kGalSmallName = "k_gal_small";
 constexpr const char* kGalSmallInitName = "k_gal_small_init";
 
@@ -1663,6 +1913,23 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_iter");
     }
+    static int psf_rows_state(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kPsfRowsName, 1), st);
+        const int bpg = (a.h / 2 + G::LPB - 1) / G::LPB;
+        hipLaunchKernelGGL((k_psf_rows<L, true>), dim3(a.N * bpg), dim3(256), 0, st, a);
+        return check_launch("k_psf_rows");
+    }
+    template <int KM>
+    static int gal_init_v(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalInitName, KM), st);
+        if constexpr (KM == 2) {
+            hipLaunchKernelGGL((k_gal_w1<L>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
+            return check_launch("k_gal_w1");
+        } else {
+            hipLaunchKernelGGL((k_gal_iter<L, false, false, KM>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
+            return check_launch("k_gal_iter");
+        }
+    }
     template <bool FIRST, bool LAST>
     static int gal_iter2_v(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kGalIter2Name, FIRST + 2 * LAST), st);
@@ -1718,6 +1985,7 @@ size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations through k_gal_iter where a size has it
+int g_fused_init = 1;  // Gaussian init through k_gal_iter<KM = 1, 2> where a size has it
 
 struct PipeRes {
     bool ok = false;
@@ -1846,6 +2114,13 @@ struct Ops {
         // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
         if constexpr (L <= 96) {
             if (g_fused) return Lc::gal_small_init(a0, st0);  // both spectra in LDS, one pass
+        }
+        if constexpr (has_fused<L>()) {
+            if (g_fused_init && a0.h <= 64) {  // whole-galaxy passes, no workspace: PSF rows -> U1 slot, init, W~
+                GD_TRY(Lc::psf_rows_state(a0, st0));
+                GD_TRY(Lc::template gal_init_v<1>(a0, st0));
+                return Lc::template gal_init_v<2>(a0, st0);
+            }
         }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
@@ -1987,7 +2262,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.10"; }
+const char* gd_engine_rev(void) { return "r01.11"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2304,6 +2579,12 @@ size_t gd_set_chunk_bytes(size_t bytes) {
 int gd_set_pipeline_streams(int streams) {
     const int old = g_pipe_streams;
     if (streams >= 1) g_pipe_streams = streams < kMaxPipe ? streams : kMaxPipe;
+    return old;
+}
+
+int gd_set_fused_init(int on) {
+    const int old = g_fused_init;
+    g_fused_init = on ? 1 : 0;
     return old;
 }
 

@@ -168,6 +168,13 @@ int gd_set_pipeline_streams(int streams);
  * setting; process-wide. */
 int gd_set_fused_iteration(int on);
 
+/* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
+ * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 three
+ * launches over the whole batch - the PSF's row spectra into the state's U1 slot, one workgroup per
+ * galaxy for y -> |H|^2, G, x0 = clamp(X0) -> zin, one for F(x0) -> W~ - with no workspace traffic.
+ * on = 0 selects the chunked chain.  Returns the previous setting; process-wide. */
+int gd_set_fused_init(int on);
+
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,
  * the SubNet kernel) on the caller's stream; level 2 also brackets every kernel launch on its own
  * stream (adds two event records per launch - under pipelining that perturbs what it measures).

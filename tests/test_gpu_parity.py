@@ -396,3 +396,62 @@ def test_pipelined_chunks_bit_identical(dev):
         lib.gd_set_chunk_bytes(old)
     for r, o in zip(ref, got):
         assert torch.equal(r, o)
+
+
+def _gauss_state_parts(st):
+    """(|H|^2, G, W~) of an ADMMState's Gaussian state buffer (U1 excluded: the fused init parks the
+    PSF's row spectra and spilled registers there before iteration 0 writes it)."""
+    N, K, L = st.N, st.W // 2 + 1, st.H
+    spec = N * K * L
+    f = st.state.view(torch.float32)
+    hh = f[:spec].view(N, K, L)
+    c = f[spec:].view(-1, 2)
+    return hh, c[:spec].reshape(N, K, L, 2), c[2 * spec:3 * spec].reshape(N, K, L, 2)
+
+
+@pytest.mark.parametrize("h", [48, 32, 64])
+def test_fused_init_matches_chunked_chain(dev, h):
+    """k_psf_rows<TO_STATE> + k_gal_iter<KM=1> (y -> |H|^2, G, x0 = clamp -> zin) + k_gal_iter<KM=2>
+    (F(x0) -> W~) against the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain: the
+    whole Gaussian state and zin, per-galaxy PSFs / alpha / rho2, ragged batch (37)."""
+    from gdeconv import _lib, engine
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 37
+    obs, psf, alpha, _ = make_batch(N, 256, h=h, seed=90 + h, device=dev)
+    r2 = (0.5 + torch.rand(N, generator=torch.Generator().manual_seed(h))).to(dev)
+    outs = []
+    old = lib.gd_set_fused_init(1)
+    try:
+        for on in (1, 0):
+            lib.gd_set_fused_init(on)
+            st = engine.ADMMState(obs, psf, alpha, "Gaussian")
+            st.state.fill_(0)
+            st.init((r2, 1))
+            torch.cuda.synchronize()
+            outs.append([t.clone().cpu() for t in (*_gauss_state_parts(st), st.zin)])
+    finally:
+        lib.gd_set_fused_init(old)
+    (hh_f, g_f, w_f, z_f), (hh_c, g_c, w_c, z_c) = outs
+    for a, b, name in ((hh_f, hh_c, "|H|^2"), (g_f, g_c, "G"), (w_f, w_c, "W~"), (z_f, z_c, "zin")):
+        e = nerr(a.reshape(N, -1), b.reshape(N, -1))
+        print(f"h={h} {name}: fused vs chunked {e:.2e}")
+        assert e < 5e-6, name
+    assert float(z_f.min()) >= 0.0 and float(z_f.max()) <= 1.0
+
+
+@pytest.mark.parametrize("fused_init", [1, 0])
+def test_admm256_fused_init_end_to_end(dev, fused_init):
+    """The whole identity-denoiser forward with either init against the reference's golden output."""
+    from gdeconv import _lib
+    lib = _lib.load()
+    g = golden("admm256_id.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    m = _spectral_model(8, "Gaussian", dev, T(g["Gaussian_rho1"]), T(g["Gaussian_rho2"]))
+    old = lib.gd_set_fused_init(fused_init)
+    try:
+        with torch.no_grad():
+            out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    finally:
+        lib.gd_set_fused_init(old)
+    assert nerr(out, T(g["Gaussian_out"])) < TOL
