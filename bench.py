@@ -37,6 +37,9 @@ MODE_NAMES = {
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES"],
     "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
+    "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],
+    "k_gal_init": ["-", "Y", "W1"],
+    "k_psf_rows": ["ROWS", "STATE"],
 }
 
 
@@ -47,7 +50,8 @@ def pretty(name):
         return f"op_richardson_lucy<{L}>"
     if k.startswith("op_"):
         return f"{k}<{L},{['Gaussian', 'Poisson'][int(mode)]}>"
-    return f"{k}<{L},{MODE_NAMES[k][int(mode)]}>"
+    names = MODE_NAMES.get(k)
+    return f"{k}<{L},{names[int(mode)]}>" if names and int(mode) < len(names) else name
 
 
 def op_bytes(name, L, n_iters, fused=False):

@@ -29,13 +29,18 @@ MODE_NAMES = {
 def pretty(kname):
     if "k_subnet_features" in kname:
         return "k_subnet_features<128,FEATURES>"
-    m = re.search(r"(k_gal_iter2?)<(\d+), (true|false), (true|false)>", kname)
+    m = re.search(r"(k_gal_iter2?)<(\d+), (true|false), (true|false)(?:, (\d+))?>", kname)
     if m:
+        if m.group(5) == "1":
+            return f"k_gal_init<{m.group(2)},Y>"      # fused init: y -> |H|^2, G, zin
         first, last = m.group(3) == "true", m.group(4) == "true"
         return f"{m.group(1)}<{m.group(2)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
-    m = re.search(r"k_psf_rows<(\d+)>", kname)
+    m = re.search(r"k_gal_w1<(\d+)>", kname)
     if m:
-        return f"k_psf_rows<{m.group(1)},ROWS>"
+        return f"k_gal_init<{m.group(1)},W1>"         # fused init: zin -> W~
+    m = re.search(r"k_psf_rows<(\d+)(, (true|false))?>", kname)
+    if m:
+        return f"k_psf_rows<{m.group(1)},{'STATE' if m.group(3) == 'true' else 'ROWS'}>"
     m = re.search(r"(k_\w+)<(\d+), (\d+)(?:, \d+)?>", kname)
     if not m:
         return None
@@ -92,6 +97,12 @@ def main():
             "hbm_bytes_per_launch": tot / a.iters, "launches": a.iters,
             "note": "sum over the iteration's RF/C/RI chunk launches; FETCH/WRITE_SIZE count L2<->fabric "
                     "traffic, Infinity-Cache hits included"}
+    init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
+    if all(k in out["kernels"] for k in init):
+        out["kernels"][f"op_admm_init<{L},Gaussian>"] = {
+            "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in init),
+            "launches": out["kernels"][init[1]]["launches"],
+            "note": "fused init: k_psf_rows<STATE> + k_gal_iter<KM=1> + k_gal_w1, per call"}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out["kernels"].items():
         if "read_bytes_per_launch" in v:
