@@ -666,6 +666,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
 #ifndef GD_FUSED_GROUP
 #define GD_FUSED_GROUP 4
 #endif
+#ifndef GD_FUSED_LPARK
+#define GD_FUSED_LPARK 2  // parked values per thread kept in the LDS left over (16 KiB) instead of global
+#endif
 #ifndef GD_ITER2_PARKA
 #define GD_ITER2_PARKA 1  // k_gal_iter2: park column A's second half in global memory during column B
 #endif
@@ -915,6 +918,11 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     // (KM = 1 parks in zin, its output)
     float2* park0 = reinterpret_cast<float2*>((KM == 1 ? a.o2 : a.o0) + (size_t)g * L * L);
     float2* park1 = park0 + (size_t)L * L / 4;
+    // The LDS the union leaves free holds LP values per thread: slice B's register RB0 (both pairs)
+    // during column A, then column A's results s < LP during column B (the former are restored first).
+    constexpr int LP = GD_FUSED_LPARK;
+    static_assert(LP == 0 || LP == FG::PPL, "one LDS-parked register per pair");
+    __shared__ float2 parkL[LP ? LP : 1][FG::THREADS];
     constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
     constexpr int NPB = GD_FUSED_NPB;                   // of which parked
     static_assert(NPB <= RB1 - RB0 && FG::PPL * NPB * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4,
@@ -922,7 +930,12 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-        for (int r = RB0; r < RB0 + NPB; ++r) park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
+        for (int r = RB0; r < RB0 + NPB; ++r) {
+            if (LP && r == RB0)
+                parkL[q][tid] = X[q][r];
+            else
+                park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
+        }
     lds_barrier();  // exchange areas -> slice A
     GD_TRACE(2);
 
@@ -1005,8 +1018,17 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
 #pragma unroll
         for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
     }
+    if constexpr (LP > 0) {
 #pragma unroll
-    for (int s = 0; s < F2; ++s) park1[s * FG::THREADS + tid] = C[s];
+        for (int q = 0; q < FG::PPL; ++q) X[q][RB0] = parkL[q][opaque(tid)];
+    }
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        if (s < LP)
+            parkL[s][tid] = C[s];
+        else
+            park1[s * FG::THREADS + tid] = C[s];
+    }
     lds_barrier();  // exchange areas -> slice B
     GD_TRACE(5);
 
@@ -1014,7 +1036,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q)
 #pragma unroll
-        for (int r = RB0; r < RB0 + NPB; ++r) X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
+        for (int r = RB0 + (LP ? 1 : 0); r < RB0 + NPB; ++r)
+            X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
         float2* row = S + (line + LINES * q) * SLD;
@@ -1055,7 +1078,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
 #pragma unroll
         for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
             float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
-            const float2 c = park1[s * FG::THREADS + opaque(tid)];
+            const float2 c = s < LP ? parkL[s < LP ? s : 0][opaque(tid)] : park1[s * FG::THREADS + opaque(tid)];
             rr[line] = make_float2(c.x, l0 ? 0.f : c.y);  // column 0: real part (irfft)
             rr[KS + line] = Cb[s];
         }
@@ -2262,7 +2285,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.11"; }
+const char* gd_engine_rev(void) { return "r01.12"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
