@@ -76,15 +76,39 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
         const int oy = p / SO, ox = p - oy * SO;
         float res[CPT];
         if constexpr (POOL) {
+            // the 2 x 2 conv outputs under one pool window share a 4 x 4 input window: 16 LDS reads
+            // per input channel instead of 4 x 9 (same fma order per output as conv_pixel)
+            float acc[4][CPT];
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) res[k] = 0.f;   // ReLU outputs are >= 0
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float acc[CPT];
-                conv_pixel<CIN, CPT, S>(in, w, b, c0, 2 * oy + (q >> 1), 2 * ox + (q & 1), acc);
+                for (int k = 0; k < CPT; ++k) acc[q][k] = b[c0 + k];
+            const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+#pragma unroll 2
+            for (int ci = 0; ci < CIN; ++ci) {
+                float win[4][4];
 #pragma unroll
-                for (int k = 0; k < CPT; ++k) res[k] = fmaxf(res[k], acc[k]);
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int yy = y0 + r, xx = x0 + c;
+                        win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
+                    }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+                            for (int k = 0; k < CPT; ++k)
+                                acc[q][k] = fmaf(w[(((c0 + k) * CIN + ci) * 3 + dy) * 3 + dx],
+                                                 win[(q >> 1) + dy][(q & 1) + dx], acc[q][k]);
             }
+#pragma unroll
+            for (int k = 0; k < CPT; ++k)   // ReLU outputs are >= 0
+                res[k] = fmaxf(fmaxf(fmaxf(0.f, acc[0][k]), fmaxf(0.f, acc[1][k])),
+                               fmaxf(fmaxf(0.f, acc[2][k]), fmaxf(0.f, acc[3][k])));
         } else {
             conv_pixel<CIN, CPT, S>(in, w, b, c0, oy, ox, res);
 #pragma unroll
