@@ -153,6 +153,9 @@ def parse():
     p.add_argument("--chunk-mb", type=float, default=None,
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
+    p.add_argument("--fused-init", type=int, default=None,
+                   help="Gaussian init at 256^2: 1 one launch (k_gal_iter<KM=3>), 2 k_gal_iter<KM=1> + k_gal_w1, "
+                        "0 chunked five-kernel chain")
     p.add_argument("--fused", type=int, default=None, help="2: one-kernel Gaussian iteration with register transposes, 1: one-kernel with parking (256^2), 0: three kernels")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
@@ -223,6 +226,10 @@ def main():
     lib.gd_set_chunk_bytes(chunk_bytes)
     if args.fused is not None:
         lib.gd_set_fused_iteration(args.fused)
+    if args.fused_init is not None:
+        lib.gd_set_fused_init(args.fused_init)
+    fused_init = lib.gd_set_fused_init(1)
+    lib.gd_set_fused_init(fused_init)
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
     use_fused = bool(fused) and args.size == 256 and args.llh == "Gaussian"
@@ -403,7 +410,11 @@ def main():
                    "iteration": ({1: "fused (k_gal_iter, one workgroup per galaxy)",
                                   2: "fused (k_gal_iter2, register transpose, one workgroup per galaxy)"}[fused]
                                  if use_fused else ("whole RL loop per Infinity-Cache chunk (RIF/C chain)" if rl
-                                                    else "three-kernel"))},
+                                                    else "three-kernel")),
+                   "init": (None if rl else
+                            {1: "fused, one launch (k_psf_rows + k_gal_iter<KM=3>)",
+                             2: "fused, two launches (k_psf_rows + k_gal_iter<KM=1> + k_gal_w1)"}.get(fused_init, "chunked")
+                            if (L == 256 and args.llh == "Gaussian") else "per-size default")},
         "roofline": roofline,
         "engine_hbm": {"survey_bytes_per_galaxy": survey_b, "achieved_GBs_per_gpu": engine_gbs,
                        "frac_of_peak": engine_gbs / HBM_PEAK_GBS},

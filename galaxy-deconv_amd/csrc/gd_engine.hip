@@ -867,291 +867,18 @@ __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<
     }
 }
 
-template <int L, bool FIRST, bool LAST, int KM = 0>
-__global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
-    using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, ALD = FG::ALD, LINES = FG::LINES;
-    constexpr float inv_n = float(1.0 / double(L * L));
-    __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
-    __shared__ float nyqo[L];       // x(., L/2)
-    __shared__ float2 nyqh[KM == 1 ? L : 1];  // init: the OTF's Nyquist column
-    static_assert(KM == 0 || (KM == 1 && !FIRST && !LAST), "init variant");
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
-    const bool l0 = (line == 0);
-    float2* my = S + line * FG::XCH;
-    fill_twiddles<L>(tw, tid, FG::THREADS);
-    const float r1 = KM == 0 ? a.rho1(g) : 0.f, r2 = KM == 0 ? a.rho2(g) : 0.f;
-    const float r2n = (LAST || KM != 0) ? 0.f : a.rho2n(g);
-    const float al = KM == 1 ? a.alpha(g) : 1.f;
-    GD_TRACE(0);
-
-    // R: pair p = line + LINES q  (KM = 1: max(y,0)/alpha, RF_YA)
-    float2 X[FG::PPL][F2];
-    {
-        const float* z = (KM == 0 ? a.a0 : a.y) + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) {
-                if constexpr (KM == 1)
-                    X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
-                else
-                    X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
-            }
-        }
-    }
-    __syncthreads();  // twiddles; all of z loaded (zin may alias z: the park stores below write it)
-    GD_TRACE(1);
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
-    // Register budget (128 VGPRs at 1024 threads; a column's FFTs and update take ~92): what a later
-    // phase needs beyond that is parked in this galaxy's output image, written whole at the end:
-    // region 0 = part of slice B's bins (registers r in [RB0, RB0 + NPB)), region 1 = column A's
-    // results.  Lane-contiguous (512 B per wave instruction),
-    // read back by the same thread; every parked value is read back (and consumed into LDS) before
-    // phase I writes that part of the image.
-    // (KM = 1 parks in zin, its output)
-    float2* park0 = reinterpret_cast<float2*>((KM == 1 ? a.o2 : a.o0) + (size_t)g * L * L);
-    float2* park1 = park0 + (size_t)L * L / 4;
-    // The LDS the union leaves free holds LP values per thread: slice B's register RB0 (both pairs)
-    // during column A, then column A's results s < LP during column B (the former are restored first).
-    constexpr int LP = GD_FUSED_LPARK;
-    static_assert(LP == 0 || LP == FG::PPL, "one LDS-parked register per pair");
-    __shared__ float2 parkL[LP ? LP : 1][FG::THREADS];
-    constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
-    constexpr int NPB = GD_FUSED_NPB;                   // of which parked
-    static_assert(NPB <= RB1 - RB0 && FG::PPL * NPB * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4,
-                  "park regions");
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q)
-#pragma unroll
-        for (int r = RB0; r < RB0 + NPB; ++r) {
-            if (LP && r == RB0)
-                parkL[q][tid] = X[q][r];
-            else
-                park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
-        }
-    lds_barrier();  // exchange areas -> slice A
-    GD_TRACE(2);
-
-    // A: bins of columns 0..KS-1 and the Nyquist bins
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        const int p = line + LINES * q;
-        float2* row = S + p * SLD;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            const int k = j + F1 * r;
-            if (r < KS / F1) row[k] = X[q][r];                               // X_p[kx], kx = k
-            if (r == 0 && j == 0) row[KS] = X[q][r];                          // X_p[L - 0]
-            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];                  // X_p[L/2]
-            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
-        }
-    }
-    lds_barrier();
-    GD_TRACE(3);
-    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);  // column A's first bins: in flight under gather + FFT
-    // Columns 0 and L/2 are real sequences over the rows (Re / Im of the pairs' X_p[0], X_p[L/2]):
-    // line 0 carries both as one complex column Z = c_0 + i c_{L/2}, splits the spectra after the
-    // forward FFT (C_0 = (Z + conj Z(-ky))/2, C_{L/2} = (Z - conj Z(-ky))/2i), updates column 0 itself
-    // and hands column L/2 to the first L/64 waves, one element per thread; the results are packed
-    // back the same way, so the inverse FFT's real / imaginary parts are x(., 0) and x(., L/2) (only
-    // real parts are kept for the self-conjugate row bins, as irfft does).
-    float2 Hc[KM == 1 ? F2 : 1];
-    float2 C[F2];
-    fused_gather<L>(S, line, j, C);
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const int y = j + F1 * s;
-        const float2 w = nyq[y >> 1];
-        if (l0) C[s].y = (y & 1) ? w.y : w.x;
-    }
-    lds_barrier();  // S -> exchange areas
-    GD_TRACE(4);
-    line_fft<L, false, true>(C, opaque(j), my, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) my[j + F1 * s] = C[s];
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int ky = j + F1 * s;
-            const float2 z = C[s], zm = my[(L - ky) & (L - 1)];
-            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
-            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-        }
-        wave_lds_sync();  // (the inverse FFT rewrites the exchange area)
-    }
-    if constexpr (KM == 1) {
-        stash<L>(my, C, j);
-        init_hload<L>(a, Hc, g, line, j);
-        init_hfft<L>(Hc, j, l0, tw, nyqh);
-    }
-    lds_barrier();  // nyqc (nyqh) complete
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
-        const size_t on = ((size_t)g * FG::K + L / 2) * L + tid;
-        if constexpr (KM == 0)
-            nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
-        else
-            nyqc[tid] = init_bin(a, on, nyqc[tid], nyqh[tid], al, inv_n);
-    }
-    if constexpr (KM == 0) {
-        fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
-    } else {
-        unstash<L>(my, C, j);
-        init_update<L, KM>(a, C, Hc, g, line, j, al, r2n);
-    }
-    lds_barrier();  // Nyquist results
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const float2 cn = nyqc[j + F1 * s];
-        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
-    }
-    line_fft<L, true, true>(C, opaque(j), my, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
-    }
-    if constexpr (LP > 0) {
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) X[q][RB0] = parkL[q][opaque(tid)];
-    }
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        if (s < LP)
-            parkL[s][tid] = C[s];
-        else
-            park1[s * FG::THREADS + tid] = C[s];
-    }
-    lds_barrier();  // exchange areas -> slice B
-    GD_TRACE(5);
-
-    // B: columns KS..2KS-1
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q)
-#pragma unroll
-        for (int r = RB0 + (LP ? 1 : 0); r < RB0 + NPB; ++r)
-            X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        float2* row = S + (line + LINES * q) * SLD;
-#pragma unroll
-        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
-            const int k = j + F1 * r;
-            if (r < 2 * KS / F1) row[k - KS] = X[q][r];                       // X_p[kx], kx = k
-            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
-                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];        // X_p[L - kx] at KS + (kx - KS)
-            }
-        }
-    }
-    lds_barrier();
-    GD_TRACE(6);
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
-    float2 Cb[F2];
-    fused_gather<L>(S, line, j, Cb);
-    lds_barrier();
-    GD_TRACE(7);
-    line_fft<L, false, true>(Cb, opaque(j), my, tw);
-    if constexpr (KM == 0) {
-        fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
-    } else {
-        stash<L>(my, Cb, j);
-        init_hload<L>(a, Hc, g, KS + line, j);
-        init_hfft<L>(Hc, j, false, tw, nyqh);
-        unstash<L>(my, Cb, j);
-        init_update<L, KM>(a, Cb, Hc, g, KS + line, j, al, r2n);
-    }
-    line_fft<L, true, true>(Cb, opaque(j), my, tw);
-
-    // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
-    // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
-    float* out = (KM == 1 ? a.o2 : a.o0) + (size_t)g * L * L;
-    static_for<0, 2>([&](auto hfc) {
-        constexpr int hf = decltype(hfc)::value;
-        lds_barrier();  // exchange areas -> row half spectra
-#pragma unroll
-        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
-            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
-            const float2 c = s < LP ? parkL[s < LP ? s : 0][opaque(tid)] : park1[s * FG::THREADS + opaque(tid)];
-            rr[line] = make_float2(c.x, l0 ? 0.f : c.y);  // column 0: real part (irfft)
-            rr[KS + line] = Cb[s];
-        }
-        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        lds_barrier();
-        float2 V[F2];
-        {
-            const int jj = opaque(j);
-            const float2* re = S + (2 * opaque(line)) * SLD;
-            const float2* ro = re + SLD;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) {
-                const int k = jj + F1 * r;
-                float2 be, bo;
-                if (k <= L / 2) {
-                    be = re[k];
-                    bo = ro[k];
-                } else {
-                    be = cconj(re[L - k]);
-                    bo = cconj(ro[L - k]);
-                }
-                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
-            }
-        }
-        lds_barrier();  // row half spectra -> exchange areas
-        line_fft<L, true, true>(V, j, my, tw);
-        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            if constexpr (KM == 1) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
-                o[F1 * r] = fminf(fmaxf(V[r].x, 0.f), 1.f);
-                o[L + F1 * r] = fminf(fmaxf(V[r].y, 0.f), 1.f);
-            } else {
-                o[F1 * r] = V[r].x;
-                o[L + F1 * r] = V[r].y;
-            }
-        }
-        GD_TRACE(8 + hf);
-    });
-}
-
-// Iteration 0's W~ for the fused init (C_G_W1's arithmetic: W~ = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2))
-// without parking: no inverse follows, so once column A is gathered into registers, slice B's bins
-// go straight from the row FFTs' registers into S, and column A is transformed with register (DPP)
-// transposes while S holds them.  Moves x0 = zin, |H|^2, G in and W~ out (3.5 words per pixel).
+// W~'s columns (k_gal_w1) from x0's row spectra in registers (X[q] = pairs line + LINES q): slice A
+// -> S, column A gathered, slice B -> S, column A by register transposes, column B.  S, nyq, nyqc
+// are the caller's LDS (the fused-iteration layout); the caller's exchange areas must be free.
 template <int L>
-__global__ __launch_bounds__(1024) void k_gal_w1(Args a) {
+__device__ __forceinline__ void w1_columns(const Args& a, float2 (&X)[FusedGeo<L>::PPL][FusedGeo<L>::F2], float2* S,
+                                           float2* nyq, float2* nyqc, const float2* tw, int g, int tid) {
     using FG = FusedGeo<L>;
     constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
-    static_assert(F1 == 16 && F2 == 16, "register transposes for 16 x 16 lines");
-    __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // line 0's split scratch, then the Nyquist column's spectrum
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
+    const int line = tid / F1, j = tid - line * F1;
     const bool l0 = (line == 0);
     float2* my = S + line * FG::XCH;
-    fill_twiddles<L>(tw, tid, FG::THREADS);
     const float r2n = a.rho2n(g);
-    float2 X[FG::PPL][F2];
-    {
-        const float* z = a.o2 + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
-        }
-    }
-    __syncthreads();  // twiddles
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
     lds_barrier();  // exchange areas -> slice A
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
@@ -1220,6 +947,298 @@ __global__ __launch_bounds__(1024) void k_gal_w1(Args a) {
     lds_barrier();  // S -> exchange areas
     line_fft<L, false, true>(C, opaque(j), my, tw);
     init_update<L, 2>(a, C, dummy, g, KS + line, j, 1.f, r2n);
+}
+
+template <int L, bool FIRST, bool LAST, int KM = 0>
+__global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
+    using FG = FusedGeo<L>;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, ALD = FG::ALD, LINES = FG::LINES;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
+    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
+    __shared__ float nyqo[L];       // x(., L/2)
+    __shared__ float2 nyqh[(KM & 1) ? L : 1];  // init: the OTF's Nyquist column
+    static_assert(KM == 0 || ((KM == 1 || KM == 3) && !FIRST && !LAST), "init variants");
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * FG::XCH;
+    fill_twiddles<L>(tw, tid, FG::THREADS);
+    const float r1 = KM == 0 ? a.rho1(g) : 0.f, r2 = KM == 0 ? a.rho2(g) : 0.f;
+    const float r2n = (LAST || KM != 0) ? 0.f : a.rho2n(g);
+    const float al = (KM & 1) ? a.alpha(g) : 1.f;
+    GD_TRACE(0);
+
+    // R: pair p = line + LINES q  (KM = 1: max(y,0)/alpha, RF_YA)
+    float2 X[FG::PPL][F2];
+    {
+        const float* z = (KM == 0 ? a.a0 : a.y) + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                if constexpr ((KM & 1))
+                    X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
+                else
+                    X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+            }
+        }
+    }
+    __syncthreads();  // twiddles; all of z loaded (zin may alias z: the park stores below write it)
+    GD_TRACE(1);
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
+    // Register budget (128 VGPRs at 1024 threads; a column's FFTs and update take ~92): what a later
+    // phase needs beyond that is parked in this galaxy's output image, written whole at the end:
+    // region 0 = part of slice B's bins (registers r in [RB0, RB0 + NPB)), region 1 = column A's
+    // results.  Lane-contiguous (512 B per wave instruction),
+    // read back by the same thread; every parked value is read back (and consumed into LDS) before
+    // phase I writes that part of the image.
+    // (KM = 1 parks in zin, its output)
+    float2* park0 = reinterpret_cast<float2*>(((KM & 1) ? a.o2 : a.o0) + (size_t)g * L * L);
+    float2* park1 = park0 + (size_t)L * L / 4;
+    // The LDS the union leaves free holds LP values per thread: slice B's register RB0 (both pairs)
+    // during column A, then column A's results s < LP during column B (the former are restored first).
+    constexpr int LP = GD_FUSED_LPARK;
+    static_assert(LP == 0 || LP == FG::PPL, "one LDS-parked register per pair");
+    __shared__ float2 parkL[LP ? LP : 1][FG::THREADS];
+    constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
+    constexpr int NPB = GD_FUSED_NPB;                   // of which parked
+    static_assert(NPB <= RB1 - RB0 && FG::PPL * NPB * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4,
+                  "park regions");
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q)
+#pragma unroll
+        for (int r = RB0; r < RB0 + NPB; ++r) {
+            if (LP && r == RB0)
+                parkL[q][tid] = X[q][r];
+            else
+                park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
+        }
+    lds_barrier();  // exchange areas -> slice A
+    GD_TRACE(2);
+
+    // A: bins of columns 0..KS-1 and the Nyquist bins
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        const int p = line + LINES * q;
+        float2* row = S + p * SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = j + F1 * r;
+            if (r < KS / F1) row[k] = X[q][r];                               // X_p[kx], kx = k
+            if (r == 0 && j == 0) row[KS] = X[q][r];                          // X_p[L - 0]
+            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];                  // X_p[L/2]
+            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
+        }
+    }
+    lds_barrier();
+    GD_TRACE(3);
+    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);  // column A's first bins: in flight under gather + FFT
+    // Columns 0 and L/2 are real sequences over the rows (Re / Im of the pairs' X_p[0], X_p[L/2]):
+    // line 0 carries both as one complex column Z = c_0 + i c_{L/2}, splits the spectra after the
+    // forward FFT (C_0 = (Z + conj Z(-ky))/2, C_{L/2} = (Z - conj Z(-ky))/2i), updates column 0 itself
+    // and hands column L/2 to the first L/64 waves, one element per thread; the results are packed
+    // back the same way, so the inverse FFT's real / imaginary parts are x(., 0) and x(., L/2) (only
+    // real parts are kept for the self-conjugate row bins, as irfft does).
+    float2 Hc[(KM & 1) ? F2 : 1];
+    float2 C[F2];
+    fused_gather<L>(S, line, j, C);
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int y = j + F1 * s;
+        const float2 w = nyq[y >> 1];
+        if (l0) C[s].y = (y & 1) ? w.y : w.x;
+    }
+    lds_barrier();  // S -> exchange areas
+    GD_TRACE(4);
+    line_fft<L, false, true>(C, opaque(j), my, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) my[j + F1 * s] = C[s];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int ky = j + F1 * s;
+            const float2 z = C[s], zm = my[(L - ky) & (L - 1)];
+            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        }
+        wave_lds_sync();  // (the inverse FFT rewrites the exchange area)
+    }
+    if constexpr ((KM & 1)) {
+        stash<L>(my, C, j);
+        init_hload<L>(a, Hc, g, line, j);
+        init_hfft<L>(Hc, j, l0, tw, nyqh);
+    }
+    lds_barrier();  // nyqc (nyqh) complete
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
+        const size_t on = ((size_t)g * FG::K + L / 2) * L + tid;
+        if constexpr (KM == 0)
+            nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
+        else
+            nyqc[tid] = init_bin(a, on, nyqc[tid], nyqh[tid], al, inv_n);
+    }
+    if constexpr (KM == 0) {
+        fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
+    } else {
+        unstash<L>(my, C, j);
+        init_update<L, 1>(a, C, Hc, g, line, j, al, r2n);
+    }
+    lds_barrier();  // Nyquist results
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const float2 cn = nyqc[j + F1 * s];
+        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
+    }
+    line_fft<L, true, true>(C, opaque(j), my, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
+    }
+    if constexpr (LP > 0) {
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q) X[q][RB0] = parkL[q][opaque(tid)];
+    }
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        if (s < LP)
+            parkL[s][tid] = C[s];
+        else
+            park1[s * FG::THREADS + tid] = C[s];
+    }
+    lds_barrier();  // exchange areas -> slice B
+    GD_TRACE(5);
+
+    // B: columns KS..2KS-1
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q)
+#pragma unroll
+        for (int r = RB0 + (LP ? 1 : 0); r < RB0 + NPB; ++r)
+            X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) {
+        float2* row = S + (line + LINES * q) * SLD;
+#pragma unroll
+        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
+            const int k = j + F1 * r;
+            if (r < 2 * KS / F1) row[k - KS] = X[q][r];                       // X_p[kx], kx = k
+            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
+                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];        // X_p[L - kx] at KS + (kx - KS)
+            }
+        }
+    }
+    lds_barrier();
+    GD_TRACE(6);
+    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
+    float2 Cb[F2];
+    fused_gather<L>(S, line, j, Cb);
+    lds_barrier();
+    GD_TRACE(7);
+    line_fft<L, false, true>(Cb, opaque(j), my, tw);
+    if constexpr (KM == 0) {
+        fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
+    } else {
+        stash<L>(my, Cb, j);
+        init_hload<L>(a, Hc, g, KS + line, j);
+        init_hfft<L>(Hc, j, false, tw, nyqh);
+        unstash<L>(my, Cb, j);
+        init_update<L, 1>(a, Cb, Hc, g, KS + line, j, al, r2n);
+    }
+    line_fft<L, true, true>(Cb, opaque(j), my, tw);
+
+    // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
+    // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
+    float* out = ((KM & 1) ? a.o2 : a.o0) + (size_t)g * L * L;
+    float2 Xw[KM == 3 ? FG::PPL : 1][F2];  // KM = 3: row spectra of the clamped x0 (W~'s input)
+    static_for<0, 2>([&](auto hfc) {
+        constexpr int hf = decltype(hfc)::value;
+        lds_barrier();  // exchange areas -> row half spectra
+#pragma unroll
+        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
+            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
+            const float2 c = s < LP ? parkL[s < LP ? s : 0][opaque(tid)] : park1[s * FG::THREADS + opaque(tid)];
+            rr[line] = make_float2(c.x, l0 ? 0.f : c.y);  // column 0: real part (irfft)
+            rr[KS + line] = Cb[s];
+        }
+        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        lds_barrier();
+        float2 V[F2];
+        {
+            const int jj = opaque(j);
+            const float2* re = S + (2 * opaque(line)) * SLD;
+            const float2* ro = re + SLD;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                const int k = jj + F1 * r;
+                float2 be, bo;
+                if (k <= L / 2) {
+                    be = re[k];
+                    bo = ro[k];
+                } else {
+                    be = cconj(re[L - k]);
+                    bo = cconj(ro[L - k]);
+                }
+                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+        lds_barrier();  // row half spectra -> exchange areas
+        line_fft<L, true, true>(V, j, my, tw);
+        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            if constexpr ((KM & 1)) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
+                const float2 c = make_float2(fminf(fmaxf(V[r].x, 0.f), 1.f), fminf(fmaxf(V[r].y, 0.f), 1.f));
+                o[F1 * r] = c.x;
+                o[L + F1 * r] = c.y;
+                if constexpr (KM == 3) Xw[KM == 3 ? hf : 0][r] = c;
+            } else {
+                o[F1 * r] = V[r].x;
+                o[L + F1 * r] = V[r].y;
+            }
+        }
+        if constexpr (KM == 3) line_fft<L, false, true>(Xw[KM == 3 ? hf : 0], j, my, tw);  // F(x0) rows
+        GD_TRACE(8 + hf);
+    });
+    if constexpr (KM == 3) w1_columns<L>(a, Xw, S, nyq, nyqc, tw, g, tid);
+}
+
+// Iteration 0's W~ for the fused init (C_G_W1's arithmetic: W~ = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2))
+// without parking: no inverse follows, so once column A is gathered into registers, slice B's bins
+// go straight from the row FFTs' registers into S, and column A is transformed with register (DPP)
+// transposes while S holds them.  Moves x0 = zin, |H|^2, G in and W~ out (3.5 words per pixel).
+template <int L>
+__global__ __launch_bounds__(1024) void k_gal_w1(Args a) {
+    using FG = FusedGeo<L>;
+    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
+    static_assert(F1 == 16 && F2 == 16, "register transposes for 16 x 16 lines");
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
+    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // line 0's split scratch, then the Nyquist column's spectrum
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * FG::XCH;
+    fill_twiddles<L>(tw, tid, FG::THREADS);
+    float2 X[FG::PPL][F2];
+    {
+        const float* z = a.o2 + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < FG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+        }
+    }
+    __syncthreads();  // twiddles
+#pragma unroll
+    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
+    w1_columns<L>(a, X, S, nyq, nyqc, tw, g, tid);
 }
 
 // No-park variant (gd_set_fused_iteration(2)): the column transforms use the register (DPP) transpose,
@@ -2008,7 +2027,7 @@ size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations through k_gal_iter where a size has it
-int g_fused_init = 1;  // Gaussian init through k_gal_iter<KM = 1, 2> where a size has it
+int g_fused_init = 1;  // Gaussian init: 1 = k_gal_iter<KM = 3> (one launch), 2 = <KM = 1> + k_gal_w1, 0 = chunked
 
 struct PipeRes {
     bool ok = false;
@@ -2141,8 +2160,11 @@ struct Ops {
         if constexpr (has_fused<L>()) {
             if (g_fused_init && a0.h <= 64) {  // whole-galaxy passes, no workspace: PSF rows -> U1 slot, init, W~
                 GD_TRY(Lc::psf_rows_state(a0, st0));
-                GD_TRY(Lc::template gal_init_v<1>(a0, st0));
-                return Lc::template gal_init_v<2>(a0, st0);
+                if (g_fused_init == 2) {
+                    GD_TRY(Lc::template gal_init_v<1>(a0, st0));
+                    return Lc::template gal_init_v<2>(a0, st0);
+                }
+                return Lc::template gal_init_v<3>(a0, st0);
             }
         }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
@@ -2285,7 +2307,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.12"; }
+const char* gd_engine_rev(void) { return "r01.13"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2607,7 +2629,7 @@ int gd_set_pipeline_streams(int streams) {
 
 int gd_set_fused_init(int on) {
     const int old = g_fused_init;
-    g_fused_init = on ? 1 : 0;
+    g_fused_init = (on == 1 || on == 2) ? on : 0;
     return old;
 }
 

@@ -409,11 +409,13 @@ def _gauss_state_parts(st):
     return hh, c[:spec].reshape(N, K, L, 2), c[2 * spec:3 * spec].reshape(N, K, L, 2)
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("h", [48, 32, 64])
-def test_fused_init_matches_chunked_chain(dev, h):
-    """k_psf_rows<TO_STATE> + k_gal_iter<KM=1> (y -> |H|^2, G, x0 = clamp -> zin) + k_gal_iter<KM=2>
-    (F(x0) -> W~) against the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain: the
-    whole Gaussian state and zin, per-galaxy PSFs / alpha / rho2, ragged batch (37)."""
+def test_fused_init_matches_chunked_chain(dev, h, variant):
+    """k_psf_rows<TO_STATE> + k_gal_iter<KM=3> (one launch: y -> |H|^2, G, x0 = clamp -> zin, F(x0) ->
+    W~) or k_gal_iter<KM=1> + k_gal_w1 (two launches) against the chunked RF_YA -> psf_rows -> C_G_INIT
+    -> RIF_CLAMP -> C_G_W1 chain: the whole Gaussian state and zin, per-galaxy PSFs / alpha / rho2,
+    ragged batch (37)."""
     from gdeconv import _lib, engine
     from gdeconv.synth import make_batch
     lib = _lib.load()
@@ -423,7 +425,7 @@ def test_fused_init_matches_chunked_chain(dev, h):
     outs = []
     old = lib.gd_set_fused_init(1)
     try:
-        for on in (1, 0):
+        for on in (variant, 0):
             lib.gd_set_fused_init(on)
             st = engine.ADMMState(obs, psf, alpha, "Gaussian")
             st.state.fill_(0)
@@ -435,12 +437,12 @@ def test_fused_init_matches_chunked_chain(dev, h):
     (hh_f, g_f, w_f, z_f), (hh_c, g_c, w_c, z_c) = outs
     for a, b, name in ((hh_f, hh_c, "|H|^2"), (g_f, g_c, "G"), (w_f, w_c, "W~"), (z_f, z_c, "zin")):
         e = nerr(a.reshape(N, -1), b.reshape(N, -1))
-        print(f"h={h} {name}: fused vs chunked {e:.2e}")
+        print(f"h={h} v={variant} {name}: fused vs chunked {e:.2e}")
         assert e < 5e-6, name
     assert float(z_f.min()) >= 0.0 and float(z_f.max()) <= 1.0
 
 
-@pytest.mark.parametrize("fused_init", [1, 0])
+@pytest.mark.parametrize("fused_init", [1, 2, 0])
 def test_admm256_fused_init_end_to_end(dev, fused_init):
     """The whole identity-denoiser forward with either init against the reference's golden output."""
     from gdeconv import _lib
