@@ -396,6 +396,44 @@ struct ColTraits {
 #ifndef GD_RCP_DIV
 #define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % k_gal_iter time)
 #endif
+// Streaming (single-use per iteration) state traffic: GD_NT marks it non-temporal (experiment switch;
+// measured: op_admm_iter 1.663 -> 1.715 ms, i.e. slower - off).
+#ifndef GD_NT
+#define GD_NT 0
+#endif
+__device__ __forceinline__ float ld_s(const float* p) {
+#if GD_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float2 ld_s(const float2* p) {
+#if GD_NT
+    const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
+    float2 r;
+    __builtin_memcpy(&r, &v, 8);
+    return r;
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void st_s(float* p, float v) {
+#if GD_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_s(float2* p, float2 v) {
+#if GD_NT
+    unsigned long long u;
+    __builtin_memcpy(&u, &v, 8);
+    __builtin_nontemporal_store(u, reinterpret_cast<unsigned long long*>(p));
+#else
+    *p = v;
+#endif
+}
 struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the variant skips them)
     float hh;
     float2 G, U1, W;
@@ -403,12 +441,12 @@ struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the va
 template <bool FIRST, bool LAST>
 __device__ __forceinline__ GState gauss_load(const Args& a, size_t o) {
     GState st;
-    st.hh = a.s_hh[o];
+    st.hh = ld_s(a.s_hh + o);
     st.G = make_float2(0.f, 0.f);
     st.U1 = make_float2(0.f, 0.f);
-    if constexpr (!LAST) st.G = a.s_g[o];
-    if constexpr (!FIRST) st.U1 = a.s_u1[o];
-    st.W = a.s_w[o];
+    if constexpr (!LAST) st.G = ld_s(a.s_g + o);
+    if constexpr (!FIRST) st.U1 = ld_s(a.s_u1 + o);
+    st.W = ld_s(a.s_w + o);
     return st;
 }
 template <bool FIRST, bool LAST>
@@ -437,8 +475,8 @@ __device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 
     const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
 #endif
     if (valid) {
-        a.s_u1[o] = U1n;
-        a.s_w[o] = csub(Vt, U2t);
+        st_s(a.s_u1 + o, U1n);
+        st_s(a.s_w + o, csub(Vt, U2t));
     }
     return cscale(cadd(X, U1n), inv_n);
 }
@@ -983,7 +1021,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
                 if constexpr ((KM & 1))
                     X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
                 else
-                    X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
+                    X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
             }
         }
     }
@@ -1197,8 +1235,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
                 o[L + F1 * r] = c.y;
                 if constexpr (KM == 3) Xw[KM == 3 ? hf : 0][r] = c;
             } else {
-                o[F1 * r] = V[r].x;
-                o[L + F1 * r] = V[r].y;
+                st_s(o + F1 * r, V[r].x);
+                st_s(o + L + F1 * r, V[r].y);
             }
         }
         if constexpr (KM == 3) line_fft<L, false, true>(Xw[KM == 3 ? hf : 0], j, my, tw);  // F(x0) rows
