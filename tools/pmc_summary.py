@@ -33,6 +33,8 @@ def pretty(kname):
     if m:
         if m.group(5) == "1":
             return f"k_gal_init<{m.group(2)},Y>"      # fused init: y -> |H|^2, G, zin
+        if m.group(5) == "3":
+            return f"k_gal_init<{m.group(2)},ONE>"    # fused init in one launch: y -> |H|^2, G, zin, W~
         first, last = m.group(3) == "true", m.group(4) == "true"
         return f"{m.group(1)}<{m.group(2)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
     m = re.search(r"k_gal_w1<(\d+)>", kname)
@@ -98,11 +100,13 @@ def main():
             "note": "sum over the iteration's RF/C/RI chunk launches; FETCH/WRITE_SIZE count L2<->fabric "
                     "traffic, Infinity-Cache hits included"}
     init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
+    if f"k_gal_init<{L},ONE>" in out["kernels"]:
+        init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},ONE>"]
     if all(k in out["kernels"] for k in init):
         out["kernels"][f"op_admm_init<{L},Gaussian>"] = {
             "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in init),
             "launches": out["kernels"][init[1]]["launches"],
-            "note": "fused init: k_psf_rows<STATE> + k_gal_iter<KM=1> + k_gal_w1, per call"}
+            "note": "fused init: " + " + ".join(init) + ", per call"}
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out["kernels"].items():
         if "read_bytes_per_launch" in v:
