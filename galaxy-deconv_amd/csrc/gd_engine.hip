@@ -396,20 +396,24 @@ struct ColTraits {
 #ifndef GD_RCP_DIV
 #define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % k_gal_iter time)
 #endif
-// Streaming (single-use per iteration) state traffic: GD_NT marks it non-temporal (experiment switch;
-// measured: op_admm_iter 1.663 -> 1.715 ms, i.e. slower - off).
-#ifndef GD_NT
-#define GD_NT 0
+// Streaming (single-use per iteration) state traffic marked non-temporal.  Measured on op_admm_iter:
+// stores (U1, W~, zin) 1.673/1.692 -> 1.658/1.666 ms - on; loads (z, |H|^2, G, U1, W~) 1.75-1.87 ms,
+// i.e. slower - off.  The parked registers stay ordinary (they are re-read by the same CU).
+#ifndef GD_NT_LD
+#define GD_NT_LD 0
+#endif
+#ifndef GD_NT_ST
+#define GD_NT_ST 1
 #endif
 __device__ __forceinline__ float ld_s(const float* p) {
-#if GD_NT
+#if GD_NT_LD
     return __builtin_nontemporal_load(p);
 #else
     return *p;
 #endif
 }
 __device__ __forceinline__ float2 ld_s(const float2* p) {
-#if GD_NT
+#if GD_NT_LD
     const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
     float2 r;
     __builtin_memcpy(&r, &v, 8);
@@ -419,14 +423,14 @@ __device__ __forceinline__ float2 ld_s(const float2* p) {
 #endif
 }
 __device__ __forceinline__ void st_s(float* p, float v) {
-#if GD_NT
+#if GD_NT_ST
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
 #endif
 }
 __device__ __forceinline__ void st_s(float2* p, float2 v) {
-#if GD_NT
+#if GD_NT_ST
     unsigned long long u;
     __builtin_memcpy(&u, &v, 8);
     __builtin_nontemporal_store(u, reinterpret_cast<unsigned long long*>(p));
@@ -2345,7 +2349,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.13"; }
+const char* gd_engine_rev(void) { return "r01.14"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
