@@ -457,3 +457,24 @@ def test_admm256_fused_init_end_to_end(dev, fused_init):
     finally:
         lib.gd_set_fused_init(old)
     assert nerr(out, T(g["Gaussian_out"])) < TOL
+
+
+@pytest.mark.parametrize("h", [96, 48])
+def test_fused_init_shared_psf_and_large_psf(dev, h):
+    """Gaussian init through gd_admm_init with ONE shared PSF ([1,1,h,h], psf stride 0): h = 48 takes
+    the fused one-launch init, h = 96 (> 64) falls back to the chunked chain; both against the oracle."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    assert lib.gd_set_fused_init(1) in (0, 1, 2)
+    N = 5
+    obs, psf, alpha, _ = make_batch(N, 256, h=h, seed=300 + h, device=dev)
+    psf1 = psf[:1].contiguous()
+    gen = torch.Generator().manual_seed(h)
+    rho1 = (0.5 + torch.rand(N, 1, 1, 2, generator=gen)).to(dev)
+    rho2 = (0.5 + torch.rand(N, 1, 1, 2, generator=gen)).to(dev)
+    m = _spectral_model(2, "Gaussian", dev, rho1, rho2)
+    with torch.no_grad():
+        out = m(obs, psf1, alpha).cpu()
+    ref = O.admm_forward(obs.cpu(), psf1.expand(N, -1, -1, -1).cpu(), alpha.cpu(), rho1.cpu(), rho2.cpu())
+    assert nerr(out, ref) < TOL
