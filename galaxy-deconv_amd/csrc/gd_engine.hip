@@ -438,22 +438,94 @@ __device__ __forceinline__ void st_s(float2* p, float2 v) {
     *p = v;
 #endif
 }
+// Gaussian ADMM state layout (|H|^2, G, U1, W~; [N][K][L], one column of L bins per (galaxy, kx)).  At
+// L = 256 the bins inside a column are stored in the order the fused iteration's column lines hold
+// them (lane j of a 16-lane line holds ky = j + 16 s), so a lane's bins are contiguous and move with
+// 16-byte accesses (k_gal_reg): complex arrays at 32 (s >> 1) + 2 j + (s & 1), |H|^2 at 64 (s >> 2) +
+// 4 j + (s & 3).  Other sizes keep ky order.  Every kernel touching this state indexes it through
+// sidx_* / sflat_* (the state buffer is opaque to callers).
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int L>
+__device__ __forceinline__ int sidx_c(int ky) {
+    if constexpr (L == 256) {
+        const int j = ky & 15, s = ky >> 4;
+        return 32 * (s >> 1) + 2 * j + (s & 1);
+    } else {
+        return ky;
+    }
+}
+template <int L>
+__device__ __forceinline__ int sidx_h(int ky) {
+    if constexpr (L == 256) {
+        const int j = ky & 15, s = ky >> 4;
+        return 64 * (s >> 2) + 4 * j + (s & 3);
+    } else {
+        return ky;
+    }
+}
+// flat offsets o = (g K + kx) L + ky -> storage offsets (columns start at multiples of L)
+template <int L>
+__device__ __forceinline__ size_t sflat_c(size_t o) {
+    if constexpr (L == 256) return (o & ~size_t(255)) | (size_t)sidx_c<L>((int)(o & 255));
+    else return o;
+}
+template <int L>
+__device__ __forceinline__ size_t sflat_h(size_t o) {
+    if constexpr (L == 256) return (o & ~size_t(255)) | (size_t)sidx_h<L>((int)(o & 255));
+    else return o;
+}
 struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the variant skips them)
     float hh;
     float2 G, U1, W;
 };
-template <bool FIRST, bool LAST>
+template <int L, bool FIRST, bool LAST>
 __device__ __forceinline__ GState gauss_load(const Args& a, size_t o) {
     GState st;
-    st.hh = ld_s(a.s_hh + o);
+    const size_t oc = sflat_c<L>(o);
+    st.hh = ld_s(a.s_hh + sflat_h<L>(o));
     st.G = make_float2(0.f, 0.f);
     st.U1 = make_float2(0.f, 0.f);
-    if constexpr (!LAST) st.G = ld_s(a.s_g + o);
-    if constexpr (!FIRST) st.U1 = ld_s(a.s_u1 + o);
-    st.W = ld_s(a.s_w + o);
+    if constexpr (!LAST) st.G = ld_s(a.s_g + oc);
+    if constexpr (!FIRST) st.U1 = ld_s(a.s_u1 + oc);
+    st.W = ld_s(a.s_w + oc);
     return st;
 }
-template <bool FIRST, bool LAST>
+// One bin of the Gaussian iteration (the arithmetic every fused and chunked kernel shares): returns the
+// next denoiser input's bin (X on the last iteration) and the updated U1, W~ (not on the last).
+template <bool LAST>
+__device__ __forceinline__ float2 gauss_math(float hh, float2 Gk, float2 U1, float2 Wt, float2 Zk, float r1, float r2,
+                                             float r2n, float inv_n, float2& U1o, float2& Wo) {
+    const float lhs = r1 * hh + r2;
+    const float2 A = csub(Zk, U1);
+#if GD_RCP_DIV
+    const float rl = __builtin_amdgcn_rcpf(lhs);
+    const float2 X = make_float2((r1 * A.x + r2 * Wt.x) * rl, (r1 * A.y + r2 * Wt.y) * rl);
+#else
+    const float2 X = make_float2((r1 * A.x + r2 * Wt.x) / lhs, (r1 * A.y + r2 * Wt.y) / lhs);
+#endif
+    if constexpr (LAST) return cscale(X, inv_n);
+    const float2 U1n = csub(cadd(U1, X), Zk);
+    const float2 HHX = cscale(X, hh);
+    const float2 U2t = csub(HHX, Wt);
+    const float d = 1.0f + r2n;
+#if GD_RCP_DIV
+    const float rd = __builtin_amdgcn_rcpf(d);
+    const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) * rd, (r2n * (HHX.y + U2t.y) + Gk.y) * rd);
+#else
+    const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
+#endif
+    U1o = U1n;
+    Wo = csub(Vt, U2t);
+    return cscale(cadd(X, U1n), inv_n);
+}
+// gauss_math with the last-iteration choice at run time (uniform per launch): the same operations, in
+// the same order, as gauss_math<false> / <true>
+__device__ __forceinline__ float2 gauss_math_rt(float hh, float2 Gk, float2 U1, float2 Wt, float2 Zk, float r1,
+                                                float r2, float r2n, float inv_n, float2& U1o, float2& Wo, bool last) {
+    if (last) return gauss_math<true>(hh, Gk, U1, Wt, Zk, r1, r2, r2n, inv_n, U1o, Wo);
+    return gauss_math<false>(hh, Gk, U1, Wt, Zk, r1, r2, r2n, inv_n, U1o, Wo);
+}
+template <int L, bool FIRST, bool LAST>
 __device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 Zk, const GState& st, float r1,
                                                 float r2, float r2n, bool valid, float inv_n) {
     const float hh = st.hh;
@@ -479,15 +551,15 @@ __device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 
     const float2 Vt = make_float2((r2n * (HHX.x + U2t.x) + Gk.x) / d, (r2n * (HHX.y + U2t.y) + Gk.y) / d);
 #endif
     if (valid) {
-        st_s(a.s_u1 + o, U1n);
-        st_s(a.s_w + o, csub(Vt, U2t));
+        st_s(a.s_u1 + sflat_c<L>(o), U1n);
+        st_s(a.s_w + sflat_c<L>(o), csub(Vt, U2t));
     }
     return cscale(cadd(X, U1n), inv_n);
 }
-template <bool FIRST, bool LAST>
+template <int L, bool FIRST, bool LAST>
 __device__ __forceinline__ float2 gauss_iter_elem(const Args& a, size_t o, float2 Zk, float r1, float r2,
                                                   float r2n, bool valid, float inv_n) {
-    return gauss_iter_st<FIRST, LAST>(a, o, Zk, gauss_load<FIRST, LAST>(a, o), r1, r2, r2n, valid, inv_n);
+    return gauss_iter_st<L, FIRST, LAST>(a, o, Zk, gauss_load<L, FIRST, LAST>(a, o), r1, r2, r2n, valid, inv_n);
 }
 
 #ifndef GD_COL_LEAN
@@ -587,21 +659,21 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float hh = Hk2.x * Hk2.x + Hk2.y * Hk2.y;
             const float2 Gk = cmulc(P[s], Hk2);
             if (valid) {
-                a.s_hh[ob + ky] = hh;
-                a.s_g[ob + ky] = Gk;
+                a.s_hh[sflat_h<L>(ob + ky)] = hh;
+                a.s_g[sflat_c<L>(ob + ky)] = Gk;
             }
             const float lhs = hh + 1.0f / al;
             P[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
         } else if constexpr (giter) {
-            P[s] = gauss_iter_elem<gfirst, glast>(a, ob + ky, P[s], r1, r2, r2n, valid, inv_n);
+            P[s] = gauss_iter_elem<L, gfirst, glast>(a, ob + ky, P[s], r1, r2, r2n, valid, inv_n);
         } else if constexpr (MODE == C_G_W1) {
             // iteration 0's W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2): the V step
             // (models/Unrolled_ADMM.py:335-336) with Hx = H X0 and u2 = 0, premultiplied by conj(H)
-            const float hh = a.s_hh[ob + ky];
-            const float2 Gk = a.s_g[ob + ky];
+            const float hh = a.s_hh[sflat_h<L>(ob + ky)];
+            const float2 Gk = a.s_g[sflat_c<L>(ob + ky)];
             const float d0 = 1.0f + r2n;
             const float2 Wt = make_float2((r2n * (hh * P[s].x + 0.0f) + Gk.x) / d0, (r2n * (hh * P[s].y + 0.0f) + Gk.y) / d0);
-            if (valid) a.s_w[ob + ky] = Wt;
+            if (valid) a.s_w[sflat_c<L>(ob + ky)] = Wt;
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
@@ -775,7 +847,7 @@ __device__ __forceinline__ void fused_prefetch(const Args& a, GState (&pre)[NPRE
     using FG = FusedGeo<L>;
     const size_t ob = ((size_t)g * FG::K + opaque(kx)) * L + opaque(j);
 #pragma unroll
-    for (int s = 0; s < NPRE; ++s) pre[s] = gauss_load<FIRST, LAST>(a, ob + FG::F1 * s);
+    for (int s = 0; s < NPRE; ++s) pre[s] = gauss_load<L, FIRST, LAST>(a, ob + FG::F1 * s);
     __builtin_amdgcn_sched_barrier(0);  // issue them here
 }
 template <int L, bool FIRST, bool LAST, int NPRE = GD_FUSED_PRE>
@@ -792,10 +864,10 @@ __device__ __forceinline__ void fused_update(const Args& a, float2 (&C)[FusedGeo
 #pragma unroll
     for (int s = 0; s < FG::F2; ++s) {
         if (s < NPRE)
-            C[s] = gauss_iter_st<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], pre[s < NPRE ? s : 0], r1, r2, r2n, true,
+            C[s] = gauss_iter_st<L, FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], pre[s < NPRE ? s : 0], r1, r2, r2n, true,
                                               inv_n);
         else
-            C[s] = gauss_iter_elem<FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
+            C[s] = gauss_iter_elem<L, FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
         if (s >= NPRE && (s - NPRE) % GD_FUSED_GROUP == GD_FUSED_GROUP - 1)
             __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
     }
@@ -874,20 +946,22 @@ __device__ __forceinline__ void unstash(const float2* my, float2 (&C)[FusedGeo<L
 }
 // init_l2 (models/Unrolled_ADMM.py:170-175) per bin: |H|^2, G = conj(H) F(max(y,0)/alpha) kept as
 // state; returns X0 / L^2 = G / (|H|^2 + 1/alpha) / L^2 (the arithmetic of k_col<C_G_INIT>)
+template <int L>
 __device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, float2 Hk, float al, float inv_n) {
     const float hh = Hk.x * Hk.x + Hk.y * Hk.y;
     const float2 Gk = cmulc(Yk, Hk);
-    a.s_hh[o] = hh;
-    a.s_g[o] = Gk;
+    a.s_hh[sflat_h<L>(o)] = hh;
+    a.s_g[sflat_c<L>(o)] = Gk;
     const float lhs = hh + 1.0f / al;
     return cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
 }
 // iteration 0's W~ (k_col<C_G_W1>'s arithmetic): the V step (:335-336) with Hx = H X0, u2 = 0, times conj(H)
+template <int L>
 __device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk, float r2n) {
-    const float hh = a.s_hh[o];
-    const float2 Gk = a.s_g[o];
+    const float hh = a.s_hh[sflat_h<L>(o)];
+    const float2 Gk = a.s_g[sflat_c<L>(o)];
     const float d0 = 1.0f + r2n;
-    a.s_w[o] = make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
+    a.s_w[sflat_c<L>(o)] = make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
 }
 template <int L, int KM>
 __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<L>::F2],
@@ -902,9 +976,9 @@ __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<
 #pragma unroll
     for (int s = 0; s < FG::F2; ++s) {
         if constexpr (KM == 1)
-            C[s] = init_bin(a, ob + FG::F1 * s, C[s], Hc[s], al, inv_n);
+            C[s] = init_bin<L>(a, ob + FG::F1 * s, C[s], Hc[s], al, inv_n);
         else
-            w1_bin(a, ob + FG::F1 * s, C[s], r2n);
+            w1_bin<L>(a, ob + FG::F1 * s, C[s], r2n);
         if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -982,7 +1056,7 @@ __device__ __forceinline__ void w1_columns(const Args& a, float2 (&X)[FusedGeo<L
     }
     lds_barrier();  // nyqc and slice B complete
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        w1_bin(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r2n);
+        w1_bin<L>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r2n);
     const float2 dummy[1] = {make_float2(0.f, 0.f)};
     init_update<L, 2>(a, C, dummy, g, line, j, 1.f, r2n);
     fused_gather<L>(S, line, j, C);
@@ -1121,9 +1195,9 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
         const size_t on = ((size_t)g * FG::K + L / 2) * L + tid;
         if constexpr (KM == 0)
-            nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
+            nyqc[tid] = gauss_iter_elem<L, FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
         else
-            nyqc[tid] = init_bin(a, on, nyqc[tid], nyqh[tid], al, inv_n);
+            nyqc[tid] = init_bin<L>(a, on, nyqc[tid], nyqh[tid], al, inv_n);
     }
     if constexpr (KM == 0) {
         fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
@@ -1385,7 +1459,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     }
     lds_barrier();  // nyqc complete; slice B complete in S
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        nyqc[tid] = gauss_iter_elem<FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
+        nyqc[tid] = gauss_iter_elem<L, FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
                                                  true, inv_n);
     fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
     lds_barrier();  // Nyquist results
@@ -1477,6 +1551,8 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
     });
 }
 
+#include "gd_galreg.hpp"  // k_gal_reg: the 512-thread, register-resident fused iteration
+
 // Small-image helpers (L <= 128, spectra in LDS as D[kx][ky]):
 // a line's forward-FFT result (packed rows r, r+1) -> the two rows' half spectra, via the line's own
 // exchange area (F1 (F2 + 1) >= L + 2 for every plan)
@@ -1559,7 +1635,7 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
         line_fft<L, false>(v, j, my, tw);
         const size_t ob = ((size_t)g * K + kx) * L + j;
 #pragma unroll
-        for (int s = 0; s < F2; ++s) v[s] = gauss_iter_elem<FIRST, LAST>(a, ob + F1 * s, v[s], r1, r2, r2n, true, inv_n);
+        for (int s = 0; s < F2; ++s) v[s] = gauss_iter_elem<L, FIRST, LAST>(a, ob + F1 * s, v[s], r1, r2, r2n, true, inv_n);
         line_fft<L, true>(v, j, my, tw);
 #pragma unroll
         for (int s = 0; s < F2; ++s) S[kx * L + j + F1 * s] = v[s];
@@ -1886,6 +1962,7 @@ constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
 constexpr const char* kGalIterName = "k_gal_iter";
 constexpr const char* kGalIter2Name = "k_gal_iter2";
+constexpr const char* kGalRegName = "k_gal_reg";
 constexpr const char* kGalInitName = "k_gal_init";
 constexpr const char* kGalSmallName = "k_gal_small";
 constexpr const char* kGalSmallInitName = "k_gal_small_init";
@@ -2035,7 +2112,13 @@ struct Launcher {
         if (a.first) return a.last ? gal_small_v<true, true>(a, st) : gal_small_v<true, false>(a, st);
         return a.last ? gal_small_v<false, true>(a, st) : gal_small_v<false, false>(a, st);
     }
+    static int gal_reg(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalRegName, a.first + 2 * a.last), st);
+        hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_reg");
+    }
     static int gal_iter(const Args& a, hipStream_t st, int variant) {
+        if (variant == 1) return gal_reg(a, st);
         if (variant == 2) {
             if (a.first) return a.last ? gal_iter2_v<true, true>(a, st) : gal_iter2_v<true, false>(a, st);
             return a.last ? gal_iter2_v<false, true>(a, st) : gal_iter2_v<false, false>(a, st);
@@ -2068,7 +2151,7 @@ struct Launcher {
 size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk; 0 = one pass
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
-int g_fused = 1;  // Gaussian iterations through k_gal_iter where a size has it
+int g_fused = 1;  // Gaussian iterations at 256^2: 1 = k_gal_reg, 2 = k_gal_iter2, 3 = k_gal_iter (parking); 0 = chunked
 int g_fused_init = 1;  // Gaussian init: 1 = k_gal_iter<KM = 3> (one launch), 2 = <KM = 1> + k_gal_w1, 0 = chunked
 
 struct PipeRes {
@@ -2341,6 +2424,7 @@ inline Args base_args(int N, void* ws, int L) {
 }  // namespace gd
 
 using namespace gd;
+#ifndef GD_KERNELS_ONLY  // tools/*.hip build single kernels without the host library
 
 // ====================================================================== C ABI
 extern "C" {
@@ -2349,7 +2433,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r01.14"; }
+const char* gd_engine_rev(void) { return "r02.1"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2677,7 +2761,7 @@ int gd_set_fused_init(int on) {
 
 int gd_set_fused_iteration(int on) {
     const int old = g_fused;
-    g_fused = (on == 1 || on == 2) ? on : 0;
+    g_fused = (on >= 1 && on <= 3) ? on : 0;
     return old;
 }
 
@@ -2695,3 +2779,4 @@ int gd_subnet_features(const void* otf128_half, const float* params, float* feat
 }  // extern "C"
 
 #include "gd_ingest.hpp"  // host-side packed-batch reader (C ABI gd_pack_*)
+#endif  // GD_KERNELS_ONLY

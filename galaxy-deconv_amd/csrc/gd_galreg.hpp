@@ -1,0 +1,414 @@
+// Register-resident whole-galaxy Gaussian iteration (k_gal_reg<256>).
+//
+// Same arithmetic, in the same order, as k_gal_iter (row FFTs of packed row pairs, column FFT +
+// spectral update + inverse column FFT per slice of 64 columns, inverse row FFTs per half of the rows;
+// results agree to rounding - the compiler contracts multiply-adds differently per kernel).  What
+// changes is the geometry and where the galaxy waits between phases:
+//   * 512 threads per workgroup (two waves per SIMD): a wave owns 256 VGPRs instead of 128;
+//   * the column FFTs use register (DPP) transposes, so once a slice has been gathered into the lines'
+//     registers the 135 KiB slice area S is free: slice B's row bins wait there during column A, and
+//     column A's results during column B.  Nothing round-trips through global memory (k_gal_iter parks
+//     2 x 131 KiB per galaxy in the output image: +23 % over the algorithmic 7.5 words per pixel);
+//   * the state is read and written with 16-byte accesses in a column order matching the lines'
+//     registers (GD_STATE_V4 below), with D groups of 4 bins in flight per wave during the update.
+//
+//   R  pair p = line + 32 q (q < 4) = rows 2p, 2p+1: z -> 4 packed row FFTs per line (LDS exchange)
+//   A  slice A's bins (columns 0..63 and the mirrored bins) -> S; each line gathers columns line and
+//      line + 32 (line 0 packs column 0 with the real Nyquist column L/2); slice B's bins -> S; column
+//      FFTs, Gaussian update against |H|^2, G, U1, W~ (models/Unrolled_ADMM.py:207-213, DESIGN.md
+//      section 2), inverse column FFTs
+//   B  slice B's bins S -> registers -> slice layout in S, gather, column A's results -> S, the same
+//      per column, column A's results back
+//   I  per half of the rows: both slices' results -> S as row half spectra, 2 inverse row FFTs per
+//      line, store zin = x + u1 (x on the last iteration)
+// Included inside namespace gd by gd_engine.hip (uses its Args, state helpers and FFT lines).
+
+// Values the compiler must materialise here: machine sinking would otherwise move the tail of a row
+// FFT (whose outputs phase B consumes) past the phase barriers, into the column phases.
+__device__ __forceinline__ void pin4(float2& a, float2& b, float2& c, float2& d) {
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(b.x), "+v"(b.y), "+v"(c.x), "+v"(c.y), "+v"(d.x), "+v"(d.y));
+}
+template <int N>
+__device__ __forceinline__ void pin(float2 (&v)[N]) {
+    static_assert(N % 4 == 0, "pin in fours");
+#pragma unroll
+    for (int i = 0; i < N; i += 4) pin4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+}
+
+// ---- 16-byte state access.  At 256^2 the Gaussian state's bins inside a column are stored in the
+// order the column lines hold them, so a lane's bins are contiguous (gd_engine.hip: sidx_c / sidx_h,
+// used by every kernel that touches this state): lane j's bins ky = j + 16 s at 32 (s >> 1) + 2 j +
+// (s & 1) (complex arrays; two bins per 16-byte access) and 64 (s >> 2) + 4 j + (s & 3) (|H|^2; four
+// bins per access).  Offsets within one galaxy's array, in elements:
+__device__ __forceinline__ int soff_c(int kx, int m, int j) { return kx * 256 + 32 * m + 2 * j; }  // bins j + 16 (2m + e)
+__device__ __forceinline__ int soff_h(int kx, int q, int j) { return kx * 256 + 64 * q + 4 * j; }  // bins j + 16 (4q + e)
+__device__ __forceinline__ f4v ld4v(const void* p) { return *reinterpret_cast<const f4v*>(p); }
+__device__ __forceinline__ void st4v(void* p, f4v v) {
+#if GD_NT_ST
+    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#else
+    *reinterpret_cast<f4v*>(p) = v;
+#endif
+}
+
+// the Nyquist column, one bin per thread (ky = tid)
+template <int L>
+__device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float2 Zk, float r1, float r2, float r2n,
+                                             bool first, bool last) {
+    constexpr float inv_n = float(1.0 / double(L * L));
+    const size_t cb = ((size_t)g * (L / 2 + 1) + L / 2) * L;
+    const int pc = sidx_c<L>(ky);
+    const float hh = a.s_hh[cb + sidx_h<L>(ky)];
+    const float2 Gk = last ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
+    const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
+    const float2 Wt = a.s_w[cb + pc];
+    float2 U1n, Wn;
+    const float2 r = gauss_math_rt(hh, Gk, U1, Wt, Zk, r1, r2, r2n, inv_n, U1n, Wn, last);
+    if (!last) {
+        st_s(a.s_u1 + cb + pc, U1n);
+        st_s(a.s_w + cb + pc, Wn);
+    }
+    return r;
+}
+
+// A line's NC columns (C[u]: kx0 + kstep u) as one stream of 4 NC groups of 4 bins, the state loads
+// of D groups ahead in flight while a group is computed (memory-level parallelism per wave).
+#ifndef GD_REG_DEPTH
+#define GD_REG_DEPTH 2
+#endif
+
+struct SGroup {
+    f4v h, g[2], u[2], w[2];
+};
+template <int L>
+__device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb, int kx, int q, int j, bool first,
+                                            bool last) {
+    G.h = ld4v(a.s_hh + gb + soff_h(kx, q, j));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const size_t off = gb + soff_c(kx, 2 * q + h, j);
+        G.g[h] = last ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);
+        G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_u1 + off);
+        G.w[h] = ld4v(a.s_w + off);
+    }
+}
+template <int L, int NC, int D = GD_REG_DEPTH>
+__device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16], int g, int kx0, int kstep, int j,
+                                               float r1, float r2, float r2n, bool first, bool last) {
+    constexpr float inv_n = float(1.0 / double(L * L));
+    constexpr int NG = 4 * NC;
+    j = opaque(j);
+    kx0 = opaque(kx0);
+    __builtin_amdgcn_sched_barrier(0);
+    const size_t gb = (size_t)g * (L / 2 + 1) * L;
+    SGroup G[NG];
+#pragma unroll
+    for (int t = 0; t < D && t < NG; ++t) sgroup_load<L>(a, G[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < NG; ++t) {
+        const int u = t / 4, q = t % 4;
+        f4v uo[2], wo[2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int h = e >> 1, c = 2 * (e & 1);
+            float2 U1n, Wn;
+            C[u][4 * q + e] = gauss_math_rt(G[t].h[e], make_float2(G[t].g[h][c], G[t].g[h][c + 1]),
+                                            make_float2(G[t].u[h][c], G[t].u[h][c + 1]),
+                                            make_float2(G[t].w[h][c], G[t].w[h][c + 1]), C[u][4 * q + e], r1, r2, r2n,
+                                            inv_n, U1n, Wn, last);
+            uo[h][c] = U1n.x; uo[h][c + 1] = U1n.y;
+            wo[h][c] = Wn.x; wo[h][c + 1] = Wn.y;
+        }
+        if (!last) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const size_t off = gb + soff_c(kx0 + kstep * u, 2 * q + h, j);
+                st4v(a.s_u1 + off, uo[h]);
+                st4v(a.s_w + off, wo[h]);
+            }
+        }
+        if (t + D < NG) sgroup_load<L>(a, G[t + D], gb, kx0 + kstep * ((t + D) / 4), (t + D) % 4, j, first, last);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// experiment switch: GD_REG_NOFFT = 1 skips every transform (memory and LDS skeleton only)
+// register-allocation switches: materialise the column transforms' outputs where they are computed
+#ifndef GD_REG_PINF
+#define GD_REG_PINF 0
+#endif
+#ifndef GD_REG_PINI
+#define GD_REG_PINI 0
+#endif
+#ifndef GD_REG_NOFFT
+#define GD_REG_NOFFT 0
+#endif
+template <int L, bool INV, bool DPP = false>
+__device__ __forceinline__ void reg_fft(float2 (&v)[16], int j, float2* xch, const float2* tw) {
+#if GD_REG_NOFFT
+    asm volatile("" ::: "memory");
+#else
+    line_fft<L, INV, true, DPP>(v, j, xch, tw);
+#endif
+}
+
+template <int L>
+struct RegGeo {
+    static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1;
+    static constexpr int THREADS = 512, LINES = THREADS / F1;  // 32 lines of 16 lanes
+    static constexpr int NP = L / 2, PPL = NP / LINES;          // 128 row pairs, 4 per line
+    static constexpr int KS = L / 4, CPL = KS / LINES;          // 64 columns per slice, 2 per line
+    static constexpr int SLD = FusedGeo<L>::SLD;                // slice layout [pair][SLD] (as k_gal_iter)
+    static constexpr int XCH = xch_elems<L>();
+    static constexpr int HPL = (NP / 2) / LINES;                // row pairs per line in a half of phase I
+    static constexpr int U = cmax(NP * SLD, LINES * XCH);
+    static constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;    // row registers [RB0, RB1] hold slice B
+    // The column transforms use the lines' LDS exchange areas (S[0, LINES XCH)); above them, S holds
+    // PK values per thread: slice B's row registers [RB0, RB0 + PXB) of every pair during column A,
+    // column A's second column's results during column B.
+    static constexpr int XA = LINES * XCH;
+    static constexpr int PK = (U - XA) / THREADS;
+    static constexpr int PXB = PK / PPL;
+    static_assert(F1 == 16 && F2 == 16 && PPL == 4 && CPL == 2 && HPL == 2, "256 x 256 geometry");
+    static_assert(SLD == 2 * KS + 4 && SLD > L / 2, "row half spectra fit a slice row");
+    static_assert(PK >= F2 && PXB >= 1 && RB0 + PXB <= RB1, "parking area above the exchange areas");
+};
+
+// Phase-locking: one galaxy per CU at a time, the same phase durations on every CU, so without an
+// offset all CUs load state together (HBM saturated) and then transform together (HBM idle).  Odd
+// workgroups of the first round start GD_REG_STAGGER microseconds late; CUs then keep the offset
+// from galaxy to galaxy.
+#ifndef GD_REG_STAGGER
+#define GD_REG_STAGGER 0
+#endif
+__device__ __forceinline__ void stagger_start(int g) {
+    if (GD_REG_STAGGER > 0 && g < 256 && (g & 1)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)GD_REG_STAGGER * 100) __builtin_amdgcn_s_sleep(32);
+    }
+}
+
+// First / last iteration as uniform runtime flags (a.first, a.last), not template variants: the MID
+// code's register allocation is spill-free, compile-time FIRST / LAST variants spilled 60-100 VGPRs.
+template <int L>
+__global__ __launch_bounds__(512) void k_gal_reg(Args a) {
+    using RG = RegGeo<L>;
+    constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
+    constexpr int RB0 = RG::RB0, RB1 = RG::RB1;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[RG::U];
+    __shared__ float2 nyq[RG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
+    __shared__ float2 nyqx[L];      // line 0's split scratch (S is occupied)
+    __shared__ float nyqo[L];       // x(., L/2)
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * RG::XCH;
+    fill_twiddles<L>(tw, tid, T);
+    const float r1 = a.rho1(g), r2 = a.rho2(g);
+    const bool first = __builtin_amdgcn_readfirstlane(a.first) != 0, last = __builtin_amdgcn_readfirstlane(a.last) != 0;
+    const float r2n = last ? 0.f : a.rho2n(g);
+    stagger_start(g);
+    GD_TRACE(0);
+
+    // R
+    float2 X[RG::PPL][F2];
+    {
+        const float* z = a.a0 + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q) {
+            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
+        }
+    }
+    __syncthreads();  // twiddles
+    GD_TRACE(1);
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q) {
+        reg_fft<L, false>(X[q], opaque(j), my, tw);
+        pin(X[q]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();  // exchange areas -> slice A
+    GD_TRACE(2);
+
+    // A: bins of columns 0..KS-1 and the Nyquist bins (k_gal_iter's slice layout)
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q) {
+        const int p = opaque(line) + LINES * q, jq = opaque(j);
+        float2* row = S + p * SLD;
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int k = jq + F1 * r;
+            if (r < KS / F1) row[k] = X[q][r];                               // X_p[kx], kx = k
+            if (r == 0 && jq == 0) row[KS] = X[q][r];                         // X_p[L - 0]
+            if (r == L / 2 / F1 && jq == 0) nyq[p] = X[q][r];                 // X_p[L/2]
+            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && jq > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    float2 CA[RG::CPL][F2];  // columns line, line + LINES of slice A; later their results
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CA[u]);
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const int y = j + F1 * s;
+        const float2 w = nyq[y >> 1];
+        if (l0) CA[0][s].y = (y & 1) ? w.y : w.x;  // line 0: column 0 + i column L/2
+    }
+    lds_barrier();  // slice A read -> exchange areas + parked slice B bins
+    // slice B's row registers r in [RB0, RB0 + PXB) wait in S above the exchange areas (thread-contiguous)
+    float2* park = S + RG::XA;
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q)
+#pragma unroll
+        for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
+    __builtin_amdgcn_sched_barrier(0);
+    GD_TRACE(3);
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) {
+        reg_fft<L, false>(CA[u], opaque(j), my, tw);
+        if (GD_REG_PINF) pin(CA[u]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqx[j + F1 * s] = CA[0][s];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int ky = j + F1 * s;
+            const float2 z = CA[0][s], zm = nyqx[(L - ky) & (L - 1)];
+            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+            CA[0][s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        }
+    }
+    lds_barrier();  // nyqc complete
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
+        nyqc[tid] = gauss_bin4<L>(a, g, tid, nyqc[tid], r1, r2, r2n, first, last);
+    }
+    fused_update4x<L, RG::CPL>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
+    lds_barrier();  // Nyquist results
+    GD_TRACE(4);
+#pragma unroll
+    for (int s = 0; s < F2; ++s) {
+        const float2 cn = nyqc[j + F1 * s];
+        if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
+    }
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) {
+        reg_fft<L, true>(CA[u], opaque(j), my, tw);
+        if (GD_REG_PINI) pin(CA[u]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = CA[0][s].y;
+    }
+    // slice B's parked bins back (each thread its own: no barrier before), then the slice layout
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q)
+#pragma unroll
+        for (int r = RB0; r < RB0 + RG::PXB; ++r) X[q][r] = park[(q * RG::PXB + r - RB0) * T + opaque(tid)];
+    lds_barrier();  // parked bins read -> slice B
+    GD_TRACE(5);
+
+    // B: columns KS..2KS-1
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q) {
+        const int jq = opaque(j);
+        float2* row = S + (opaque(line) + LINES * q) * SLD;
+#pragma unroll
+        for (int r = RB0; r <= RB1; ++r) {
+            const int k = jq + F1 * r;
+            if (r < 2 * KS / F1) row[k - KS] = X[q][r];                       // X_p[kx], kx = k
+            if (r > L / 2 / F1 || (r == L / 2 / F1 && jq > 0)) {
+                if (r < RB1 || jq == 0) row[L - k] = X[q][r];                 // X_p[L - kx] at KS + (kx - KS)
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    float2 CB[RG::CPL][F2];
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CB[u]);
+    lds_barrier();  // slice B read -> exchange areas + parked column A results (second column)
+#pragma unroll
+    for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
+    __builtin_amdgcn_sched_barrier(0);
+    GD_TRACE(6);
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) {
+        reg_fft<L, false>(CB[u], opaque(j), my, tw);
+        if (GD_REG_PINF) pin(CB[u]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    fused_update4x<L, RG::CPL>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last);
+#pragma unroll
+    for (int u = 0; u < RG::CPL; ++u) {
+        reg_fft<L, true>(CB[u], opaque(j), my, tw);
+        if (GD_REG_PINI) pin(CB[u]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int s = 0; s < F2; ++s) CA[RG::CPL - 1][s] = park[s * T + opaque(tid)];
+
+    // I: half hf = rows [hf L/2, (hf+1) L/2): both slices' results -> S as row half spectra [yl][SLD]
+    // (bins 0..L/2), inverse FFTs of the packed row pairs m = line + LINES w, store
+    float* out = a.o0 + (size_t)g * L * L;
+    static_for<0, 2>([&](auto hfc) {
+        constexpr int hf = decltype(hfc)::value;
+        lds_barrier();  // parked results / exchange areas -> row half spectra
+        GD_TRACE(7 + hf);
+#pragma unroll
+        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
+            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                const float2 c = CA[u][s];
+                rr[line + LINES * u] = (u == 0 && l0) ? make_float2(c.x, 0.f) : c;  // column 0: real part
+                rr[KS + line + LINES * u] = CB[u][s];
+            }
+        }
+        for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        lds_barrier();
+        float2 V[RG::HPL][F2];
+#pragma unroll
+        for (int w = 0; w < RG::HPL; ++w) {
+            const int jj = opaque(j);
+            const float2* re = S + (2 * (opaque(line) + LINES * w)) * SLD;
+            const float2* ro = re + SLD;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                const int k = jj + F1 * r;
+                float2 be, bo;
+                if (k <= L / 2) {
+                    be = re[k];
+                    bo = ro[k];
+                } else {
+                    be = cconj(re[L - k]);
+                    bo = cconj(ro[L - k]);
+                }
+                V[w][r] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+        lds_barrier();  // row half spectra -> exchange areas
+#pragma unroll
+        for (int w = 0; w < RG::HPL; ++w) {
+            reg_fft<L, true>(V[w], opaque(j), my, tw);
+            float* o = out + (size_t)(hf * L / 2 + 2 * (line + LINES * w)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                st_s(o + F1 * r, V[w][r].x);
+                st_s(o + L + F1 * r, V[w][r].y);
+            }
+        }
+    });
+    __syncthreads();
+    GD_TRACE(9);
+}

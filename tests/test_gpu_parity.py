@@ -117,10 +117,11 @@ def _spectral_model(n, llh, dev, rho1, rho2):
     return m
 
 
-@pytest.fixture(params=[2, 1, 0], ids=["fused_regs", "fused", "three_kernel"])
+@pytest.fixture(params=[1, 2, 3, 0], ids=["fused_reg", "fused_regs2", "fused_park", "three_kernel"])
 def fused(request):
-    """Gaussian iterations through the one-kernel whole-galaxy path (256^2; 2: register-transpose
-    k_gal_iter2, 1: parking k_gal_iter) or the three-kernel path."""
+    """Gaussian iterations through the one-kernel whole-galaxy path (256^2; 1: k_gal_reg, the default,
+    512 threads, no parking; 2: register-transpose k_gal_iter2; 3: parking k_gal_iter) or the
+    three-kernel path."""
     from gdeconv import _lib
     lib = _lib.load()
     old = lib.gd_set_fused_iteration(request.param)
@@ -138,11 +139,11 @@ def test_admm256_spectral_engine(dev, llh, fused):
     assert nerr(out, T(g[f"{llh}_out"])) < TOL
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("n", [1, 2, 3])
 def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
-    """k_gal_iter (first / middle / last variants) against the three-kernel path and the oracle, with
-    per-galaxy rho and a ragged batch."""
+    """k_gal_reg / k_gal_iter2 / k_gal_iter (first / middle / last iterations; n = 1 is first-and-last)
+    against the three-kernel path and the oracle, with per-galaxy rho and a ragged batch."""
     from gdeconv import _lib
     from gdeconv.synth import make_batch
     lib = _lib.load()

@@ -1,0 +1,205 @@
+// Standalone check + timing of the fused Gaussian iteration variants at 256^2 (no torch):
+// k_gal_iter (1024 threads, parking) against k_gal_reg (512 threads, no parking); both use the
+// engine's 256^2 state layout (sidx_c / sidx_h).  Both run
+// the same arithmetic in the same order; the compiler contracts multiply-adds differently in the two
+// kernels, so results agree to rounding (max |d| <= 1e-6 max |x| over zin and the U1 / W~ state is the
+// bar; the tool exits non-zero otherwise).  Then each variant is timed over the batch.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/kbench_reg tools/kbench_reg.hip
+//   tools/kbench_reg [N=4096] [reps=20] [noparity]  (noparity: time layout experiments that break the comparison)
+#include "../galaxy-deconv_amd/csrc/gd_engine.hip"
+
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+__global__ void k_fill(float* p, size_t n, unsigned seed, float lo, float hi) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u + seed;
+        x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15;
+        p[i] = lo + (hi - lo) * ((x & 0xffffff) / float(0x1000000));
+    }
+}
+
+template <typename F>
+float time_ms(F&& f, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    f(); CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+constexpr int L = 256, K = L / 2 + 1;
+
+struct Bufs {
+    float *z, *zin;
+    float2* state;  // |H|^2 (K L floats, padded to K L float2) | G | U1 | W~
+    Args a;
+};
+
+Bufs make(int N, float* par) {
+    const size_t img = (size_t)N * L * L, spec = (size_t)N * K * L;
+    Bufs b;
+    CK(hipMalloc(&b.z, img * 4)); CK(hipMalloc(&b.zin, img * 4));
+    CK(hipMalloc(&b.state, 4 * spec * 8));
+    memset(&b.a, 0, sizeof(b.a));
+    b.a.N = N; b.a.s_hh = (float*)b.state; b.a.s_g = b.state + spec; b.a.s_u1 = b.a.s_g + spec; b.a.s_w = b.a.s_u1 + spec;
+    b.a.a0 = b.z; b.a.o0 = b.zin;
+    b.a.alpha = b.a.rho1 = b.a.rho2 = b.a.rho2n = GalScalar{par, 1};
+    b.a.llh = GD_LLH_GAUSSIAN;
+    return b;
+}
+
+void seed(Bufs& b, int N) {
+    const size_t img = (size_t)N * L * L, spec = (size_t)N * K * L;
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, b.z, img, 1u, 0.f, 1.f);
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (float*)b.state, 8 * spec, 2u, 0.f, 1.f);
+    CK(hipMemset(b.zin, 0, img * 4));
+    CK(hipDeviceSynchronize());
+}
+
+// Streaming ceiling for one galaxy's MID traffic (z, |H|^2, G, U1, W~ in; U1, W~, zin out), float4 per
+// lane, no phases: what the memory system gives this read/write mix with one T-thread workgroup per CU
+// (LDS sized like k_gal_reg's so the residency matches).
+template <int T>
+__global__ __launch_bounds__(T) void k_stream(Args a) {
+    __shared__ float pad[35000];
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const size_t img = (size_t)L * L, spec = (size_t)K * L;
+    const f4v* z = reinterpret_cast<const f4v*>(a.a0 + g * img);
+    f4v* zin = reinterpret_cast<f4v*>(a.o0 + g * img);
+    const f4v* hh = reinterpret_cast<const f4v*>(a.s_hh + g * spec);
+    const f4v* G = reinterpret_cast<const f4v*>(a.s_g + g * spec);
+    f4v* U = reinterpret_cast<f4v*>(a.s_u1 + g * spec);
+    f4v* W = reinterpret_cast<f4v*>(a.s_w + g * spec);
+    if (tid == 0) pad[0] = 0.f;
+    for (int i = tid; i < (int)(img / 4); i += T) zin[i] = z[i] * 1.5f;
+    for (int i = tid; i < (int)(spec / 2); i += T) {
+        const f4v h = hh[i / 2];
+        const f4v gg = G[i], u = U[i], w = W[i];
+        U[i] = u + gg * h;
+        W[i] = w - gg;
+    }
+}
+
+template <bool FIRST, bool LAST>
+void launch(int variant, Args a) {
+    a.first = FIRST;
+    a.last = LAST;
+    if (variant == 0)
+        hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(1024), 0, 0, a);
+    else
+        hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(512), 0, 0, a);
+}
+void launch_v(int variant, int fl, const Args& a) {
+    switch (fl) {
+        case 0: launch<false, false>(variant, a); break;
+        case 1: launch<true, false>(variant, a); break;
+        case 2: launch<false, true>(variant, a); break;
+        default: launch<true, true>(variant, a); break;
+    }
+}
+
+double diff(const void* x, const void* y, size_t bytes) {
+    std::vector<float> hx(bytes / 4), hy(bytes / 4);
+    CK(hipMemcpy(hx.data(), x, bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hy.data(), y, bytes, hipMemcpyDeviceToHost));
+    long long n = 0, first = -1;
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < hx.size(); ++i) {
+        if (memcmp(&hx[i], &hy[i], 4)) { ++n; if (first < 0) first = (long long)i; }
+        md = fmax(md, fabs((double)hx[i] - hy[i]));
+        mx = fmax(mx, fabs((double)hx[i]));
+    }
+    if (n) printf("   max|d| %.3e  max|x| %.3e  first differing word %lld (%g vs %g)\n", md, mx, first, hx[first], hy[first]);
+    return mx > 0 ? md / mx : md;
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 4096;
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    float* par;
+    CK(hipMalloc(&par, N * 4));
+#if GD_FUSED_TRACE
+    unsigned long long* tr;  // every launch of a traced build writes stamps: set the buffer before any
+    CK(hipMalloc(&tr, (size_t)N * 16 * 8));
+    CK(hipMemset(tr, 0, (size_t)N * 16 * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace), &tr, sizeof(tr)));
+#endif
+    hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, 0, par, (size_t)N, 3u, 0.5f, 1.5f);
+    // parity on a small batch: every variant (MID, FIRST, LAST, FIRST_LAST), all outputs
+    const int Nc = N < 64 ? N : 64;
+    const size_t img = (size_t)Nc * L * L, spec = (size_t)Nc * K * L;
+    Bufs x = make(Nc, par), y = make(Nc, par);
+    int bad = 0;
+    const char* fln[] = {"MID", "FIRST", "LAST", "FIRST_LAST"};
+    for (int fl = 0; fl < 4; ++fl) {
+        seed(x, Nc); seed(y, Nc);
+        launch_v(0, fl, x.a);
+        launch_v(1, fl, y.a);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        const double dz = diff(x.zin, y.zin, img * 4), ds = diff(x.state, y.state, 4 * spec * 8);
+        printf("parity %-10s zin max|d|/max|x| %.2e, state %.2e\n", fln[fl], dz, ds);
+        bad += !(dz <= 1e-6) || !(ds <= 1e-6);
+    }
+    if (bad && !(argc > 3 && !strcmp(argv[3], "noparity"))) {
+        printf("FAIL: k_gal_reg differs from k_gal_iter\n");
+        return 1;
+    }
+    Bufs t = make(N, par);
+    seed(t, N);
+    const double img_b = L * L * 4.0, half_b = K * L * 8.0;
+    const double gb[4] = {N * (2 * img_b + 5.5 * half_b) / 1e9, N * (2 * img_b + 4.5 * half_b) / 1e9,
+                          N * (2 * img_b + 2.5 * half_b) / 1e9, N * (2 * img_b + 1.5 * half_b) / 1e9};
+    {
+        const float m5 = time_ms([&] { hipLaunchKernelGGL(k_stream<512>, dim3(N), dim3(512), 0, 0, t.a); }, reps);
+        const float m10 = time_ms([&] { hipLaunchKernelGGL(k_stream<1024>, dim3(N), dim3(1024), 0, 0, t.a); }, reps);
+        CK(hipGetLastError());
+        printf("k_stream<512>  (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m5, gb[0] / m5);
+        printf("k_stream<1024> (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m10, gb[0] / m10);
+    }
+    for (int fl = 0; fl < 3; ++fl)
+        for (int v = 0; v < 2; ++v) {
+            const float ms = time_ms([&] { launch_v(v, fl, t.a); }, reps);
+            CK(hipGetLastError());
+            printf("%-11s<256,%-5s> N=%d  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", v ? "k_gal_reg" : "k_gal_iter",
+                   fln[fl], N, ms, gb[fl] / ms, gb[fl]);
+        }
+#if GD_FUSED_TRACE
+    // per-phase durations of k_gal_reg<MID> (thread 0's s_memrealtime stamps, 100 MHz) at several batch sizes
+    const char* names[] = {"start -> z loaded", "row FFTs", "slice A -> S + gather", "column A FFT + update",
+                           "column A IFFT", "slice B -> S + gather", "column B", "I half 0", "I half 1 + drain"};
+    for (int n : {32, 256, N}) {
+        Args b = t.a;
+        b.N = n;
+        for (int v = 0; v < 2; ++v) {  // warm, then the traced launch
+            CK(hipMemset(tr, 0, (size_t)N * 16 * 8));
+            hipLaunchKernelGGL((k_gal_reg<L>), dim3(n), dim3(512), 0, 0, b);
+            CK(hipDeviceSynchronize());
+        }
+        std::vector<unsigned long long> h((size_t)n * 16);
+        CK(hipMemcpy(h.data(), tr, h.size() * 8, hipMemcpyDeviceToHost));
+        if (n == N) {  // raw stamps of the full batch for offline analysis
+            FILE* f = fopen("gpurun_out/kreg_trace.bin", "wb");
+            if (f) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
+        }
+        printf("phase trace N=%d (mean us per workgroup):\n", n);
+        double tot = 0;
+        for (int k = 0; k < 9; ++k) {
+            double s = 0;
+            for (int i = 0; i < n; ++i) s += (double)(h[i * 16 + k + 1] - h[i * 16 + k]);
+            s = s / n / 100.0;
+            tot += s;
+            printf("  %-26s %7.2f\n", names[k], s);
+        }
+        printf("  %-26s %7.2f\n", "whole workgroup", tot);
+    }
+#endif
+    return 0;
+}
