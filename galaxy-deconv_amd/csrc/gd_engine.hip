@@ -474,6 +474,18 @@ __device__ __forceinline__ size_t sflat_h(size_t o) {
     if constexpr (L == 256) return (o & ~size_t(255)) | (size_t)sidx_h<L>((int)(o & 255));
     else return o;
 }
+// Iteration 0's W~1 = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2) (the first V step, models/
+// Unrolled_ADMM.py:335-336, premultiplied by conj(H); k_col<C_G_W1>'s arithmetic).  At L = 256 it is
+// DEFERRED: the init leaves F(x0) itself in the W~ slot and the first iteration - which reads |H|^2, G
+// and that slot anyway, with rho2 = rho2[0] as the init's - forms W~1 bin by bin (the init then never
+// re-reads |H|^2 and G: 1.5 half spectra per galaxy less).  Other sizes store W~1 in the init.
+template <int L>
+constexpr bool defer_w1() { return L == 256; }
+__device__ __forceinline__ float2 w1_value(float hh, float2 Gk, float2 Xk, float r2n) {
+    const float d0 = 1.0f + r2n;
+    return make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
+}
+
 struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the variant skips them)
     float hh;
     float2 G, U1, W;
@@ -485,7 +497,7 @@ __device__ __forceinline__ GState gauss_load(const Args& a, size_t o) {
     st.hh = ld_s(a.s_hh + sflat_h<L>(o));
     st.G = make_float2(0.f, 0.f);
     st.U1 = make_float2(0.f, 0.f);
-    if constexpr (!LAST) st.G = ld_s(a.s_g + oc);
+    if constexpr (!LAST || (FIRST && defer_w1<L>())) st.G = ld_s(a.s_g + oc);
     if constexpr (!FIRST) st.U1 = ld_s(a.s_u1 + oc);
     st.W = ld_s(a.s_w + oc);
     return st;
@@ -529,7 +541,9 @@ template <int L, bool FIRST, bool LAST>
 __device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 Zk, const GState& st, float r1,
                                                 float r2, float r2n, bool valid, float inv_n) {
     const float hh = st.hh;
-    const float2 U1 = st.U1, Gk = st.G, Wt = st.W;
+    const float2 U1 = st.U1, Gk = st.G;
+    float2 Wt = st.W;
+    if constexpr (FIRST && defer_w1<L>()) Wt = w1_value(hh, Gk, st.W, r2);  // the slot holds F(x0)
     const float lhs = r1 * hh + r2;
     const float2 A = csub(Zk, U1);
 #if GD_RCP_DIV
@@ -669,11 +683,13 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         } else if constexpr (MODE == C_G_W1) {
             // iteration 0's W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2): the V step
             // (models/Unrolled_ADMM.py:335-336) with Hx = H X0 and u2 = 0, premultiplied by conj(H)
-            const float hh = a.s_hh[sflat_h<L>(ob + ky)];
-            const float2 Gk = a.s_g[sflat_c<L>(ob + ky)];
-            const float d0 = 1.0f + r2n;
-            const float2 Wt = make_float2((r2n * (hh * P[s].x + 0.0f) + Gk.x) / d0, (r2n * (hh * P[s].y + 0.0f) + Gk.y) / d0);
-            if (valid) a.s_w[sflat_c<L>(ob + ky)] = Wt;
+            if constexpr (defer_w1<L>()) {
+                if (valid) a.s_w[sflat_c<L>(ob + ky)] = P[s];  // F(x0): the first iteration forms W~1
+            } else {
+                const float hh = a.s_hh[sflat_h<L>(ob + ky)];
+                const float2 Gk = a.s_g[sflat_c<L>(ob + ky)];
+                if (valid) a.s_w[sflat_c<L>(ob + ky)] = w1_value(hh, Gk, P[s], r2n);
+            }
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
@@ -958,10 +974,13 @@ __device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, f
 // iteration 0's W~ (k_col<C_G_W1>'s arithmetic): the V step (:335-336) with Hx = H X0, u2 = 0, times conj(H)
 template <int L>
 __device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk, float r2n) {
-    const float hh = a.s_hh[sflat_h<L>(o)];
-    const float2 Gk = a.s_g[sflat_c<L>(o)];
-    const float d0 = 1.0f + r2n;
-    a.s_w[sflat_c<L>(o)] = make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
+    if constexpr (defer_w1<L>()) {
+        a.s_w[sflat_c<L>(o)] = Xk;  // F(x0): the first iteration forms W~1
+    } else {
+        const float hh = a.s_hh[sflat_h<L>(o)];
+        const float2 Gk = a.s_g[sflat_c<L>(o)];
+        a.s_w[sflat_c<L>(o)] = w1_value(hh, Gk, Xk, r2n);
+    }
 }
 template <int L, int KM>
 __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<L>::F2],
@@ -2117,6 +2136,11 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_reg");
     }
+    static int gal_reg_init(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalInitName, 4), st);
+        hipLaunchKernelGGL((k_gal_reg_init<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_reg_init");
+    }
     static int gal_iter(const Args& a, hipStream_t st, int variant) {
         if (variant == 1) return gal_reg(a, st);
         if (variant == 2) {
@@ -2152,7 +2176,8 @@ size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations at 256^2: 1 = k_gal_reg, 2 = k_gal_iter2, 3 = k_gal_iter (parking); 0 = chunked
-int g_fused_init = 1;  // Gaussian init: 1 = k_gal_iter<KM = 3> (one launch), 2 = <KM = 1> + k_gal_w1, 0 = chunked
+int g_fused_init = 1;  // Gaussian init at 256^2 (+ k_psf_rows<STATE>): 1 = k_gal_reg_init, 2 = k_gal_iter<KM = 1> +
+                       // k_gal_w1, 3 = k_gal_iter<KM = 3>; 0 = chunked
 
 struct PipeRes {
     bool ok = false;
@@ -2289,7 +2314,8 @@ struct Ops {
                     GD_TRY(Lc::template gal_init_v<1>(a0, st0));
                     return Lc::template gal_init_v<2>(a0, st0);
                 }
-                return Lc::template gal_init_v<3>(a0, st0);
+                if (g_fused_init == 3) return Lc::template gal_init_v<3>(a0, st0);
+                return Lc::gal_reg_init(a0, st0);
             }
         }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
@@ -2755,7 +2781,7 @@ int gd_set_pipeline_streams(int streams) {
 
 int gd_set_fused_init(int on) {
     const int old = g_fused_init;
-    g_fused_init = (on == 1 || on == 2) ? on : 0;
+    g_fused_init = (on >= 1 && on <= 3) ? on : 0;
     return old;
 }
 

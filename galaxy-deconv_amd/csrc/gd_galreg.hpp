@@ -59,9 +59,10 @@ __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float
     const size_t cb = ((size_t)g * (L / 2 + 1) + L / 2) * L;
     const int pc = sidx_c<L>(ky);
     const float hh = a.s_hh[cb + sidx_h<L>(ky)];
-    const float2 Gk = last ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
+    const float2 Gk = (last && !first) ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
     const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
-    const float2 Wt = a.s_w[cb + pc];
+    float2 Wt = a.s_w[cb + pc];
+    if (first) Wt = w1_value(hh, Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
     float2 U1n, Wn;
     const float2 r = gauss_math_rt(hh, Gk, U1, Wt, Zk, r1, r2, r2n, inv_n, U1n, Wn, last);
     if (!last) {
@@ -87,7 +88,7 @@ __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb,
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const size_t off = gb + soff_c(kx, 2 * q + h, j);
-        G.g[h] = last ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);
+        G.g[h] = (last && !first) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);  // first: W~1 needs G
         G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_u1 + off);
         G.w[h] = ld4v(a.s_w + off);
     }
@@ -113,10 +114,11 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
         for (int e = 0; e < 4; ++e) {
             const int h = e >> 1, c = 2 * (e & 1);
             float2 U1n, Wn;
-            C[u][4 * q + e] = gauss_math_rt(G[t].h[e], make_float2(G[t].g[h][c], G[t].g[h][c + 1]),
-                                            make_float2(G[t].u[h][c], G[t].u[h][c + 1]),
-                                            make_float2(G[t].w[h][c], G[t].w[h][c + 1]), C[u][4 * q + e], r1, r2, r2n,
-                                            inv_n, U1n, Wn, last);
+            const float2 Gk = make_float2(G[t].g[h][c], G[t].g[h][c + 1]);
+            float2 Wt = make_float2(G[t].w[h][c], G[t].w[h][c + 1]);
+            if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
+            C[u][4 * q + e] = gauss_math_rt(G[t].h[e], Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt,
+                                            C[u][4 * q + e], r1, r2, r2n, inv_n, U1n, Wn, last);
             uo[h][c] = U1n.x; uo[h][c + 1] = U1n.y;
             wo[h][c] = Wn.x; wo[h][c + 1] = Wn.y;
         }
@@ -411,4 +413,321 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     });
     __syncthreads();
     GD_TRACE(9);
+}
+
+// ==================================================================== fused Gaussian init at 256^2
+// k_gal_reg_init: init_l2 (models/Unrolled_ADMM.py:170-175) and iteration 0's W~ (the first V step,
+// :335-336, premultiplied by conj(H)) in ONE launch on k_gal_reg's skeleton, one 512-thread workgroup
+// per galaxy (the arithmetic of k_col<C_G_INIT>, RIF_CLAMP and k_col<C_G_W1>, bin for bin):
+//   R  max(y, 0) / alpha -> 4 packed row FFTs per line
+//   A  per column of slice A: Y's column FFT; the OTF column from the PSF's compact row spectra
+//      (k_psf_rows<L, true> left them in the U1 slot) and its FFT; |H|^2, G = conj(H) Y -> state,
+//      X0 = G / (|H|^2 + 1/alpha); inverse column FFT
+//   B  the same for slice B
+//   I  per half of the rows: row IFFTs, x0 = clamp(., 0, 1) -> zin, and the clamped rows' FFTs again
+//   W  F(x0)'s columns (slice A, slice B) -> the W~ slot; iteration 0 forms W~1 = (rho2 |H|^2 F(x0) +
+//      G) / (1 + rho2) from it (defer_w1: |H|^2 and G are not re-read here)
+// Bytes per galaxy: y, zin (2 img) + |H|^2, G, F(x0) (2.5 half) + the PSF's compact rows (h (L/2 + 1)
+// complex).  No parking, 16-byte state accesses.
+
+// One column of the init (NC = 1 per call): |H|^2, G -> state; C <- X0 / L^2
+template <int L>
+__device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], const float2 (&Hc)[16], int g, int kx,
+                                             int j, float al) {
+    constexpr float inv_n = float(1.0 / double(L * L));
+    j = opaque(j);
+    kx = opaque(kx);
+    __builtin_amdgcn_sched_barrier(0);
+    const size_t gb = (size_t)g * (L / 2 + 1) * L;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f4v h4, g4[2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int s = 4 * q + e, h = e >> 1, c = 2 * (e & 1);
+            const float2 Hk = Hc[s];
+            const float hh = Hk.x * Hk.x + Hk.y * Hk.y;  // init_bin's arithmetic
+            const float2 Gk = cmulc(C[s], Hk);
+            h4[e] = hh;
+            g4[h][c] = Gk.x;
+            g4[h][c + 1] = Gk.y;
+            const float lhs = hh + 1.0f / al;
+            C[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+        }
+        *reinterpret_cast<f4v*>(a.s_hh + gb + soff_h(kx, q, j)) = h4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) *reinterpret_cast<f4v*>(a.s_g + gb + soff_c(kx, 2 * q + h, j)) = g4[h];
+    }
+}
+// One column of F(x0) (C) into the W~ slot: iteration 0 forms W~1 from it (defer_w1 at 256^2)
+template <int L>
+__device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16], int g, int kx, int j) {
+    static_assert(defer_w1<L>(), "the fused init defers W~1 to the first iteration");
+    j = opaque(j);
+    kx = opaque(kx);
+    __builtin_amdgcn_sched_barrier(0);
+    const size_t gb = (size_t)g * (L / 2 + 1) * L;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+        st4v(a.s_w + gb + soff_c(kx, m, j), f4v{C[2 * m].x, C[2 * m].y, C[2 * m + 1].x, C[2 * m + 1].y});
+}
+// The OTF column kx (FFT'd, LDS exchange) from the PSF's compact row spectra; line 0 (kx = 0, packed
+// with the real Nyquist column) splits it and leaves the Nyquist column's spectrum in nyqh.
+template <int L>
+__device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16], int g, int kx, int j, bool l0,
+                                                float2* my, const float2* tw, float2* nyqh) {
+    init_hload<L>(a, Hc, g, kx, j);
+    reg_fft<L, false>(Hc, opaque(j), my, tw);
+    if (l0) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) my[j + 16 * s] = Hc[s];
+        wave_lds_sync();
+        float2 zm[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) zm[s] = my[(L - j - 16 * s) & (L - 1)];
+        wave_lds_sync();
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const float2 z = Hc[s];
+            nyqh[j + 16 * s] = make_float2(0.5f * (z.y + zm[s].y), 0.5f * (zm[s].x - z.x));
+            Hc[s] = make_float2(0.5f * (z.x + zm[s].x), 0.5f * (z.y - zm[s].y));
+        }
+    }
+}
+
+template <int L>
+__global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
+    using RG = RegGeo<L>;
+    constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
+    constexpr int RB0 = RG::RB0, RB1 = RG::RB1;
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ __attribute__((aligned(16))) float2 S[RG::U];
+    __shared__ float2 nyq[RG::NP];  // X_p[L/2] of every pair
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
+    __shared__ float2 nyqh[L];      // the OTF's Nyquist column
+    __shared__ float nyqo[L];       // x(., L/2)
+    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
+    const int g = blockIdx.x;
+    const bool l0 = (line == 0);
+    float2* my = S + line * RG::XCH;
+    float2* park = S + RG::XA;
+    fill_twiddles<L>(tw, tid, T);
+    const float al = a.alpha(g), r2n = a.rho2n(g);
+
+    // R: max(y, 0) / alpha (RF_YA)
+    float2 X[RG::PPL][F2];
+    {
+        const float* y = a.y + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q) {
+            const float* r0 = y + (size_t)(2 * (line + LINES * q)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
+        }
+    }
+    __syncthreads();  // twiddles
+#pragma unroll
+    for (int q = 0; q < RG::PPL; ++q) {
+        reg_fft<L, false>(X[q], opaque(j), my, tw);
+        pin(X[q]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    float2 CA[RG::CPL][F2], CB[RG::CPL][F2];
+    // forward columns of the row spectra X: slice A into CA (and nyqc), slice B into CB
+    // (phase_cols is shared with the W~ pass below; INIT: the X0 columns' update and inverse)
+    auto slices = [&](auto initc) {
+        constexpr bool INIT = decltype(initc)::value;
+        lds_barrier();  // exchange areas -> slice A
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q) {
+            const int p = opaque(line) + LINES * q, jq = opaque(j);
+            float2* row = S + p * SLD;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                const int k = jq + F1 * r;
+                if (r < KS / F1) row[k] = X[q][r];
+                if (r == 0 && jq == 0) row[KS] = X[q][r];
+                if (r == L / 2 / F1 && jq == 0) nyq[p] = X[q][r];
+                if (r > (L - KS) / F1 || (r == (L - KS) / F1 && jq > 0)) row[KS + L - k] = X[q][r];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CA[u]);
+#pragma unroll
+        for (int s = 0; s < F2; ++s) {
+            const int y = j + F1 * s;
+            const float2 w = nyq[y >> 1];
+            if (l0) CA[0][s].y = (y & 1) ? w.y : w.x;
+        }
+        lds_barrier();  // slice A read -> exchange areas + parked slice B bins
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q)
+#pragma unroll
+            for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) {
+            reg_fft<L, false>(CA[u], opaque(j), my, tw);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
+#pragma unroll
+            for (int s = 0; s < F2; ++s) my[j + F1 * s] = CA[0][s];
+            wave_lds_sync();
+#pragma unroll
+            for (int s = 0; s < F2; ++s) {
+                const int ky = j + F1 * s;
+                const float2 z = CA[0][s], zm = my[(L - ky) & (L - 1)];
+                nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+                CA[0][s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+            }
+            wave_lds_sync();
+        }
+        if constexpr (INIT) {
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                float2 Hc[F2];
+                init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh);
+                init_update4<L>(a, CA[u], Hc, g, line + LINES * u, j, al);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            lds_barrier();  // nyqc, nyqh complete
+            if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
+                nyqc[tid] = init_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], nyqh[tid], al, inv_n);
+            lds_barrier();  // Nyquist results
+#pragma unroll
+            for (int s = 0; s < F2; ++s) {
+                const float2 cn = nyqc[j + F1 * s];
+                if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
+            }
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                reg_fft<L, true>(CA[u], opaque(j), my, tw);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (l0) {
+#pragma unroll
+                for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = CA[0][s].y;
+            }
+        } else {
+            lds_barrier();  // nyqc complete
+            if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
+                w1_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], r2n);
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) w1_update4<L>(a, CA[u], g, line + LINES * u, j);
+        }
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q)
+#pragma unroll
+            for (int r = RB0; r < RB0 + RG::PXB; ++r) X[q][r] = park[(q * RG::PXB + r - RB0) * T + opaque(tid)];
+        lds_barrier();  // parked bins read -> slice B
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q) {
+            const int jq = opaque(j);
+            float2* row = S + (opaque(line) + LINES * q) * SLD;
+#pragma unroll
+            for (int r = RB0; r <= RB1; ++r) {
+                const int k = jq + F1 * r;
+                if (r < 2 * KS / F1) row[k - KS] = X[q][r];
+                if (r > L / 2 / F1 || (r == L / 2 / F1 && jq > 0)) {
+                    if (r < RB1 || jq == 0) row[L - k] = X[q][r];
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CB[u]);
+        lds_barrier();  // slice B read -> exchange areas (+ parked column A results)
+        if constexpr (INIT) {
+#pragma unroll
+            for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) {
+            reg_fft<L, false>(CB[u], opaque(j), my, tw);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) {
+            if constexpr (INIT) {
+                float2 Hc[F2];
+                init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
+                init_update4<L>(a, CB[u], Hc, g, KS + line + LINES * u, j, al);
+                reg_fft<L, true>(CB[u], opaque(j), my, tw);
+            } else {
+                w1_update4<L>(a, CB[u], g, KS + line + LINES * u, j);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (INIT) {
+#pragma unroll
+            for (int s = 0; s < F2; ++s) CA[RG::CPL - 1][s] = park[s * T + opaque(tid)];
+        }
+    };
+    slices(std::true_type{});
+
+    // I: per half, row IFFTs -> x0 = clamp(., 0, 1) -> zin, then the clamped rows' FFTs (W~'s input);
+    // pair m = line + LINES w of half hf is row pair p = 64 hf + m of the W~ pass (X[2 hf + w])
+    float* out = a.o2 + (size_t)g * L * L;
+    static_for<0, 2>([&](auto hfc) {
+        constexpr int hf = decltype(hfc)::value;
+        lds_barrier();  // parked results / exchange areas -> row half spectra
+#pragma unroll
+        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
+            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                const float2 c = CA[u][s];
+                rr[line + LINES * u] = (u == 0 && l0) ? make_float2(c.x, 0.f) : c;
+                rr[KS + line + LINES * u] = CB[u][s];
+            }
+        }
+        for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        lds_barrier();
+#pragma unroll
+        for (int w = 0; w < RG::HPL; ++w) {
+            float2 (&V)[F2] = X[2 * hf + w];
+            const int jj = opaque(j);
+            const float2* re = S + (2 * (opaque(line) + LINES * w)) * SLD;
+            const float2* ro = re + SLD;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {
+                const int k = jj + F1 * r;
+                float2 be, bo;
+                if (k <= L / 2) {
+                    be = re[k];
+                    bo = ro[k];
+                } else {
+                    be = cconj(re[L - k]);
+                    bo = cconj(ro[L - k]);
+                }
+                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+        lds_barrier();  // row half spectra -> exchange areas
+#pragma unroll
+        for (int w = 0; w < RG::HPL; ++w) {
+            float2 (&V)[F2] = X[2 * hf + w];
+            reg_fft<L, true>(V, opaque(j), my, tw);
+            float* o = out + (size_t)(hf * L / 2 + 2 * (line + LINES * w)) * L + j;
+#pragma unroll
+            for (int r = 0; r < F2; ++r) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
+                V[r] = make_float2(fminf(fmaxf(V[r].x, 0.f), 1.f), fminf(fmaxf(V[r].y, 0.f), 1.f));
+                o[F1 * r] = V[r].x;
+                o[L + F1 * r] = V[r].y;
+            }
+            reg_fft<L, false>(V, opaque(j), my, tw);  // F(x0) rows
+            pin(V);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    });
+
+    // W: F(x0)'s columns -> W~ (no inverse)
+    slices(std::false_type{});
 }

@@ -163,16 +163,18 @@ size_t gd_set_chunk_bytes(size_t bytes);
 int gd_set_pipeline_streams(int streams);
 
 /* Fused Gaussian iteration: at sizes that have it (256^2) gd_admm_iter runs ONE kernel per call, one
- * workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic); on = 0 selects the
- * three-kernel path (row pass / column pass / row pass through the workspace).  Returns the previous
- * setting; process-wide. */
+ * workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic).  on: 1 = k_gal_reg
+ * (default: 512 threads, nothing parked in global memory), 2 = k_gal_iter2, 3 = k_gal_iter (1024
+ * threads, parks registers in the output image); 0 selects the three-kernel path (row pass / column
+ * pass / row pass through the workspace).  Returns the previous setting; process-wide. */
 int gd_set_fused_iteration(int on);
 
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
- * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 three
- * launches over the whole batch - the PSF's row spectra into the state's U1 slot, one workgroup per
- * galaxy for y -> |H|^2, G, x0 = clamp(X0) -> zin, one for F(x0) -> W~ - with no workspace traffic.
- * on = 0 selects the chunked chain.  Returns the previous setting; process-wide. */
+ * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
+ * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->
+ * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic.  on: 1 = k_gal_reg_init
+ * (default, one launch), 2 = k_gal_iter<KM=1> + k_gal_w1 (two launches), 3 = k_gal_iter<KM=3> (one
+ * launch, 1024 threads); 0 selects the chunked chain.  Returns the previous setting; process-wide. */
 int gd_set_fused_init(int on);
 
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,

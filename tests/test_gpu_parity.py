@@ -410,13 +410,13 @@ def _gauss_state_parts(st):
     return hh, c[:spec].reshape(N, K, L, 2), c[2 * spec:3 * spec].reshape(N, K, L, 2)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("h", [48, 32, 64])
 def test_fused_init_matches_chunked_chain(dev, h, variant):
-    """k_psf_rows<TO_STATE> + k_gal_iter<KM=3> (one launch: y -> |H|^2, G, x0 = clamp -> zin, F(x0) ->
-    W~) or k_gal_iter<KM=1> + k_gal_w1 (two launches) against the chunked RF_YA -> psf_rows -> C_G_INIT
-    -> RIF_CLAMP -> C_G_W1 chain: the whole Gaussian state and zin, per-galaxy PSFs / alpha / rho2,
-    ragged batch (37)."""
+    """k_psf_rows<TO_STATE> + k_gal_reg_init (1, the default) or k_gal_iter<KM=3> (3) (one launch: y ->
+    |H|^2, G, x0 = clamp -> zin, F(x0) -> W~) or k_gal_iter<KM=1> + k_gal_w1 (2, two launches) against the
+    chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain: the whole Gaussian state and
+    zin, per-galaxy PSFs / alpha / rho2, ragged batch (37)."""
     from gdeconv import _lib, engine
     from gdeconv.synth import make_batch
     lib = _lib.load()
