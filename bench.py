@@ -27,6 +27,29 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 TB/s measured float4 copy)
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 vector / MFMA peak (MI355X_MICROARCH.md)
+
+
+def resunet_flops(L):
+    """FLOPs of one ResUNet (models/ResUNet.py, nc = [64, 128, 256, 512], nb = 2) call on one L x L
+    galaxy: 2 x MACs of every 3x3 / 2x2 convolution and transposed convolution (biases and ReLUs
+    ignored).  141.9 GFLOP at 256^2."""
+    nc, nb, tot = [64, 128, 256, 512], 2, 0
+    def conv(cin, cout, k, hw):
+        return 2 * cin * cout * k * k * hw
+    hw = L * L
+    tot += conv(1, nc[0], 3, hw)                                  # head
+    for i in range(3):                                            # down: nb res blocks + strided 2x2
+        tot += nb * 2 * conv(nc[i], nc[i], 3, hw)
+        hw //= 4
+        tot += conv(nc[i], nc[i + 1], 2, hw)
+    tot += nb * 2 * conv(nc[3], nc[3], 3, hw)                     # body
+    for i in (2, 1, 0):                                           # up: transposed 2x2 + nb res blocks
+        hw *= 4
+        tot += 2 * nc[i + 1] * nc[i] * hw                         # transposed 2x2 / 2: one tap per output
+        tot += nb * 2 * conv(nc[i], nc[i], 3, hw)
+    tot += conv(nc[0], 1, 3, hw)                                  # tail
+    return tot
 
 # kernel mode ids (gd_engine.hip enums) -> readable names
 MODE_NAMES = {
@@ -38,9 +61,16 @@ MODE_NAMES = {
     "k_subnet_features": ["FEATURES"],
     "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],
-    "k_gal_init": ["-", "Y", "W1"],
+    "k_gal_reg": ["MID", "FIRST", "LAST", "FIRST_LAST"],
+    "k_gal_small": ["MID", "FIRST", "LAST", "FIRST_LAST"],
+    "k_gal_init": ["-", "Y", "W1", "ONE", "REG"],
     "k_psf_rows": ["ROWS", "STATE"],
 }
+# fused Gaussian iteration / init implementations (gd_set_fused_iteration / gd_set_fused_init)
+ITER_IMPL = {1: "k_gal_reg (512 threads, nothing parked in global memory)", 2: "k_gal_iter2 (register transposes)",
+             3: "k_gal_iter (1024 threads, parks registers in the output image)"}
+INIT_IMPL = {1: "k_psf_rows + k_gal_reg_init (one launch)", 2: "k_psf_rows + k_gal_iter<KM=1> + k_gal_w1",
+             3: "k_psf_rows + k_gal_iter<KM=3> (one launch)"}
 
 
 def pretty(name):
@@ -54,22 +84,36 @@ def pretty(name):
     return f"{k}<{L},{names[int(mode)]}>" if names and int(mode) < len(names) else name
 
 
-def op_bytes(name, L, n_iters, fused=False):
-    """Algorithmic bytes per galaxy of one whole engine operation (its kernels' compulsory traffic),
-    averaged over the first / middle / last ADMM iteration.  Gaussian iteration, fused (k_gal_iter):
-    z + state (|H|^2, G, U1, W~) in, U1, W~ + zin out = 2 img + 5.5 half (first: no U1 read; last: no
-    G read, no state written); three-kernel: RF(z) + C_G_ITER + RI(zin) adds the workspace round trips."""
+def op_bytes(name, L, n_iters, fused=False, h=48):
+    """Compulsory (algorithmic) HBM bytes per galaxy of one call of a whole engine operation: every
+    input the operation needs read once, every output written once, averaged
+    over the first / middle / last ADMM iteration.  This is the roofline model of every bench line;
+    the PMC 'traffic' field is what the kernels actually move.
+      op_admm_iter, Gaussian, fused (k_gal_reg, k_gal_small): z + |H|^2, G, U1, W~ in, U1, W~ + zin out
+        = 2 img + 5.5 half (first: no U1 read, 4.5; last: no G read, nothing written, 2.5; first-and-last
+        at 256^2 reads G to form W~1, 2.5); three-kernel: + the RF / C / RI workspace round trips.
+      op_admm_init, Gaussian, fused: y + PSF in, |H|^2, G, W~ (or F(x0)) + zin out = 2 img + 2.5 half
+        + the PSF (h^2 floats) and at 256^2 its compact row spectra (h (L/2 + 1) complex, written and read)."""
     img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
-    if pretty(name) == f"op_richardson_lucy<{L}>":
+    k = pretty(name)
+    if k == f"op_richardson_lucy<{L}>":
         return survey_rl_bytes_per_galaxy(L, n_iters)
-    if pretty(name) == f"op_admm_iter<{L},Gaussian>":
+    if k == f"op_admm_iter<{L},Gaussian>":
         if n == 1:
-            c = 1.5 if fused else 5.5
+            c = 2.5 if fused else 5.5
         elif fused:
             c = (4.5 + 5.5 * (n - 2) + 2.5) / n
         else:
             c = (2 + 6.5 + (2 + 7.5) * (n - 2) + 2 + 4.5) / n
         return 2 * img + c * half
+    if k == f"op_admm_init<{L},Gaussian>" and fused:
+        rows = 2 * 2 * h * (L // 2 + 1) * 8 if L == 256 else 0  # k_psf_rows<STATE>'s compact rows, out and in
+        return 2 * img + 2.5 * half + 4 * h * h + rows
+    if k == f"op_admm_iter<{L},Poisson>":
+        # u1, w (= v - u2), z in; u1, w, zin out (+ y, the OTF half spectrum); the last iteration
+        # reads z, u1, w, y, OTF and writes x only
+        mid, last = 6 * img + 2 * half, 4 * img + half
+        return (mid * (n - 1) + last) / n
     return None
 
 
@@ -145,7 +189,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=64, help="galaxies in the CPU baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--e2e-sample", type=int, default=64, help="galaxies for the ResUNet end-to-end sample")
+    p.add_argument("--e2e-sample", type=int, default=512, help="galaxies for the ResUNet end-to-end sample")
+    p.add_argument("--e2e-forwards", type=int, default=2, help="timed forwards of the end-to-end sample")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="skip the hipGraph-replay measurement")
     p.add_argument("--no-ingest", action="store_true", help="skip the packed-file ingest pipeline measurement")
@@ -154,11 +199,14 @@ def parse():
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
     p.add_argument("--fused-init", type=int, default=None,
-                   help="Gaussian init at 256^2: 1 one launch (k_gal_iter<KM=3>), 2 k_gal_iter<KM=1> + k_gal_w1, "
-                        "0 chunked five-kernel chain")
-    p.add_argument("--fused", type=int, default=None, help="2: one-kernel Gaussian iteration with register transposes, 1: one-kernel with parking (256^2), 0: three kernels")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                   help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field")
+                   help="Gaussian init at 256^2: 1 k_gal_reg_init (one launch), 2 k_gal_iter<KM=1> + k_gal_w1, "
+                        "3 k_gal_iter<KM=3>, 0 chunked five-kernel chain")
+    p.add_argument("--fused", type=int, default=None,
+                   help="Gaussian iteration: 1 k_gal_reg (256^2; k_gal_small at <= 128), 2 k_gal_iter2, "
+                        "3 k_gal_iter (parking), 0 three kernels")
+    p.add_argument("--traffic-json", default=None,
+                   help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field "
+                        "(default: profiles/pmc_traffic.json, _48 / _rl variants for those workloads)")
     return p.parse_args()
 
 
@@ -232,7 +280,7 @@ def main():
     lib.gd_set_fused_init(fused_init)
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
-    use_fused = bool(fused) and args.size == 256 and args.llh == "Gaussian"
+    use_fused = bool(fused) and args.size in (32, 48, 64, 96, 128, 256) and args.llh == "Gaussian"
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
     pipe_streams = lib.gd_set_pipeline_streams(0)
@@ -358,13 +406,21 @@ def main():
     ops = {k: v for k, v in kstats.items() if k.startswith("op_")}
     kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
     pipelined = chunk_bytes > 0
-    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused)}
+    h_psf = psf.shape[-1]
+    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused, h_psf)}
+    # every priced operation against the HBM spec (compulsory bytes / average call time)
+    for k, (ms, c) in ops.items():
+        b = op_bytes(k, L, n, use_fused, h_psf)
+        if b:
+            ach = b * N / (ms / c * 1e-3) / 1e9
+            kernels[pretty(k)].update({"algorithmic_bytes_per_call": b * N, "achieved_GBs": ach,
+                                       "frac_of_hbm_peak": ach / HBM_PEAK_GBS})
     if (pipelined or use_fused) and priced_ops:
         # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
         # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
         dom_raw = max(priced_ops, key=lambda k: ops[k][0])
         dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
-        per_gal = op_bytes(dom_raw, L, n, use_fused)
+        per_gal = op_bytes(dom_raw, L, n, use_fused, h_psf)
     else:
         priced = {k: v for k, v in kern.items() if kernel_bytes(k, L, n)} or kern
         dom_raw = max(priced, key=lambda k: kern[k][0])
@@ -372,13 +428,20 @@ def main():
         per_gal = kernel_bytes(dom_raw, L, n)
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
+    if args.traffic_json is None:
+        suffix = "_rl" if rl else ("" if L == 256 else f"_{L}")
+        args.traffic_json = os.path.join(ROOT, "profiles", f"pmc_traffic{suffix}.json")
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        ent = tj.get("kernels", {}).get(pretty(dom_raw))
         same_engine = tj.get("engine_rev") == lib.gd_engine_rev().decode()
-        if ent and same_engine and tj.get("batch") == N and tj.get("size") == L:
-            traffic = ent.get("hbm_bytes_per_launch")
+        if same_engine and tj.get("batch") == N and tj.get("size") == L and tj.get("n_iters", n) == n:
+            ent = tj.get("kernels", {}).get(pretty(dom_raw))
+            traffic = ent.get("hbm_bytes_per_launch") if ent else None
+            for k, v in kernels.items():  # PMC bytes per call beside every priced operation
+                e = tj.get("kernels", {}).get(k)
+                if e and "algorithmic_bytes_per_call" in v:
+                    v["pmc_traffic_per_call"] = e.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     roofline = {"bound": "hbm", "kernel": pretty(dom_raw), "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -386,7 +449,6 @@ def main():
                 "traffic": traffic, "algorithmic_bytes_per_launch": per_gal * N if per_gal else None,
                 "avg_launch_ms": dom_ms}
     survey_b = survey_rl_bytes_per_galaxy(L, n) if rl else survey_bytes_per_galaxy(L, n)
-    engine_gbs = survey_b * gal_s / world / 1e9
     if rl:
         metric = f"galaxies/sec ({L}x{L}, Richard_Lucy n_iters={n})"
         workload = (f"Richard_Lucy(n_iters={n}) forward (OTF + {n} multiplicative FFT-conv iterations), "
@@ -407,17 +469,22 @@ def main():
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
                    "llh": None if rl else args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
-                   "iteration": ({1: "fused (k_gal_iter, one workgroup per galaxy)",
-                                  2: "fused (k_gal_iter2, register transpose, one workgroup per galaxy)"}[fused]
+                   "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
+                                               "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
                                  if use_fused else ("whole RL loop per Infinity-Cache chunk (RIF/C chain)" if rl
                                                     else "three-kernel")),
                    "init": (None if rl else
-                            {1: "fused, one launch (k_psf_rows + k_gal_iter<KM=3>)",
-                             2: "fused, two launches (k_psf_rows + k_gal_iter<KM=1> + k_gal_w1)"}.get(fused_init, "chunked")
-                            if (L == 256 and args.llh == "Gaussian") else "per-size default")},
+                            ("fused, " + INIT_IMPL[fused_init] if fused_init else "chunked")
+                            if (L == 256 and args.llh == "Gaussian") else
+                            ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
+                             else "chunked"))},
         "roofline": roofline,
-        "engine_hbm": {"survey_bytes_per_galaxy": survey_b, "achieved_GBs_per_gpu": engine_gbs,
-                       "frac_of_peak": engine_gbs / HBM_PEAK_GBS},
+        # SURVEY.md 8(d)'s per-galaxy byte model prices the reference's op-for-op path (16 fp32 words per
+        # pixel per iteration); this engine's compulsory traffic is 7.5 (roofline above), so the survey
+        # model is reported as a reference figure only, with no fraction of peak
+        "reference_op_model": {"survey_bytes_per_galaxy": survey_b,
+                               "note": "SURVEY 8(d) byte model of the reference's per-iteration FFT round trips; "
+                                       "not this engine's traffic (see roofline / kernels.*.algorithmic_bytes_per_call)"},
         "kernels": kernels,
     }
     if gather_ms is not None:
@@ -428,6 +495,8 @@ def main():
         rec["ingest"] = ingest
 
     if rank == 0 and world == 1 and not args.no_e2e and not rl:
+        # the whole model with the ResUNet denoiser (PyTorch fp32, MIOpen, NHWC) on a sample, micro-batched
+        # by the model; priced against the fp32 MFMA peak (the denoiser's convolutions dominate)
         model.Z = denoiser
         G = min(args.e2e_sample, N)
         o2, p2, a2 = obs[:G].contiguous(), psf[:G].contiguous(), alpha[:G].contiguous()
@@ -435,11 +504,18 @@ def main():
             model(o2, p2, a2)
             torch.cuda.synchronize()
             te = time.perf_counter()
-            model(o2, p2, a2)
+            for _ in range(args.e2e_forwards):
+                model(o2, p2, a2)
             torch.cuda.synchronize()
             te = time.perf_counter() - te
-        rec["end_to_end"] = {"value": G / te, "unit": "galaxies/s",
-                             "sample": f"{G} galaxies, full model with PyTorch ResUNet (fp32, MIOpen), 1 timed forward"}
+        gal_e2e = G * args.e2e_forwards / te
+        flop_gal = resunet_flops(L) * n
+        rec["end_to_end"] = {"value": gal_e2e, "unit": "galaxies/s", "ms_per_forward": te * 1e3 / args.e2e_forwards,
+                             "denoiser_flop_per_galaxy": flop_gal,
+                             "fp32_ceiling_galaxies_s": FP32_PEAK_TFLOPS * 1e12 / flop_gal,
+                             "frac_of_fp32_ceiling": gal_e2e * flop_gal / (FP32_PEAK_TFLOPS * 1e12),
+                             "sample": f"{G} galaxies, full model with PyTorch ResUNet (fp32, MIOpen, NHWC), "
+                                       f"{args.e2e_forwards} timed forwards after one warm forward"}
         del o2, p2, a2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args)

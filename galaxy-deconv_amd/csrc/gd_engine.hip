@@ -83,6 +83,7 @@ struct Args {
     float2* Tw;            // if set: row-forward kernels write here (full-batch layout) instead of T
     const float* ltl;      // Tikhonov |L|^2 half spectrum [*][K][L] (nullptr: filter 'Identity')
     long long ltl_gstride; // elements between galaxies' |L|^2 (0 = one shared filter)
+    int otf_bcast;         // LOAD_OTF modes: one OTF for every galaxy (conv_fft_batch's broadcast H)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
@@ -645,7 +646,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
         float2 Hk = make_float2(0.f, 0.f);
-        if constexpr (TR::LOAD_OTF) Hk = a.otf[ob + ky];
+        if constexpr (TR::LOAD_OTF) Hk = a.otf[(a.otf_bcast ? (size_t)kx * L : ob) + ky];
         if constexpr (TR::STORE_OTF || MODE == C_WIENER || MODE == C_TIKHONOV) Hk = P[s];
         if constexpr (TR::STORE_OTF) {
             if (valid) a.otf[ob + ky] = Hk;
@@ -2212,7 +2213,7 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
     b.N = n;
     const size_t img = (size_t)g0 * L * L;
     const size_t spec = (size_t)g0 * (L / 2 + 1) * L;
-    if (b.otf) b.otf += spec;
+    if (b.otf && !b.otf_bcast) b.otf += spec;
     if (b.s_hh) b.s_hh += spec;
     if (b.s_g) b.s_g += spec;
     if (b.s_u1) b.s_u1 += spec;
@@ -2495,10 +2496,18 @@ int gd_psf_to_otf(const float* psf, long long psf_gstride, int h, int w, int N, 
 
 int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out, int N, int H, int W,
                       void* ws, void* stream) {
+    return gd_conv_fft_batch_strided(otf_half, (long long)(W / 2 + 1) * H, conj, x, out, N, H, W, ws, stream);
+}
+
+int gd_conv_fft_batch_strided(const void* otf_half, long long otf_gstride, int conj, const float* x, float* out,
+                              int N, int H, int W, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
+    if (otf_gstride != 0 && otf_gstride != (long long)(W / 2 + 1) * H)
+        return fail(GD_ERR_ARG, "otf_gstride must be 0 (one shared OTF) or (W/2+1)*H");
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, H);
     a.otf = reinterpret_cast<float2*>(const_cast<void*>(otf_half));
+    a.otf_bcast = otf_gstride == 0;
     a.a0 = x; a.o0 = out;
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::conv(a, conj, (hipStream_t)stream); });
 }

@@ -514,6 +514,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     float2* park = S + RG::XA;
     fill_twiddles<L>(tw, tid, T);
     const float al = a.alpha(g), r2n = a.rho2n(g);
+    GD_TRACE(0);
 
     // R: max(y, 0) / alpha (RF_YA)
     float2 X[RG::PPL][F2];
@@ -527,6 +528,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         }
     }
     __syncthreads();  // twiddles
+    GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < RG::PPL; ++q) {
         reg_fft<L, false>(X[q], opaque(j), my, tw);
@@ -539,7 +541,9 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     // (phase_cols is shared with the W~ pass below; INIT: the X0 columns' update and inverse)
     auto slices = [&](auto initc) {
         constexpr bool INIT = decltype(initc)::value;
+        constexpr int TB = INIT ? 2 : 9;  // trace stamp base
         lds_barrier();  // exchange areas -> slice A
+        GD_TRACE(TB);
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q) {
             const int p = opaque(line) + LINES * q, jq = opaque(j);
@@ -569,6 +573,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
             for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
         __builtin_amdgcn_sched_barrier(0);
+        GD_TRACE(TB + 1);
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false>(CA[u], opaque(j), my, tw);
@@ -625,6 +630,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
             for (int r = RB0; r < RB0 + RG::PXB; ++r) X[q][r] = park[(q * RG::PXB + r - RB0) * T + opaque(tid)];
         lds_barrier();  // parked bins read -> slice B
+        GD_TRACE(TB + 2);
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q) {
             const int jq = opaque(j);
@@ -643,6 +649,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CB[u]);
         lds_barrier();  // slice B read -> exchange areas (+ parked column A results)
+        GD_TRACE(TB + 3);
         if constexpr (INIT) {
 #pragma unroll
             for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
@@ -678,6 +685,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     static_for<0, 2>([&](auto hfc) {
         constexpr int hf = decltype(hfc)::value;
         lds_barrier();  // parked results / exchange areas -> row half spectra
+        GD_TRACE(6 + hf);
 #pragma unroll
         for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
             float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
@@ -729,5 +737,8 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     });
 
     // W: F(x0)'s columns -> W~ (no inverse)
+    GD_TRACE(8);
     slices(std::false_type{});
+    __syncthreads();
+    GD_TRACE(13);
 }

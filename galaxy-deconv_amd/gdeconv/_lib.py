@@ -31,6 +31,7 @@ SIGNATURES = {
     "gd_otf_bytes": (_SZ, [_I, _I, _I]),
     "gd_psf_to_otf": (_I, [_P, _LL, _I, _I, _I, _I, _I, _P, _P, _P]),
     "gd_conv_fft_batch": (_I, [_P, _I, _P, _P, _I, _I, _I, _P, _P]),
+    "gd_conv_fft_batch_strided": (_I, [_P, _LL, _I, _P, _P, _I, _I, _I, _P, _P]),
     "gd_rfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_admm_state_bytes": (_SZ, [_I, _I, _I, _I]),

@@ -6,21 +6,44 @@ library raises (``gdeconv._lib.EngineError``).
 
 Layouts: images fp32 [N,1,H,W] contiguous (NCHW, C=1, as in the reference); the OTF is the
 half spectrum stored transposed, complex64 [N, W//2+1, H] (``otf[g, kx, ky]``).
+
+Devices and streams: every entry point runs on the device of its (first) input tensor, under
+``torch.cuda.device(that device)``, and enqueues on that device's current torch stream, whatever
+the caller's current device is.  Scratch workspaces come from torch's caching allocator per call
+(on that stream), so calls on different streams or threads never share scratch memory.
 """
+import contextlib
+
 import torch
 
 from . import _lib
 
 
-def _stream():
-    return torch.cuda.current_stream().cuda_stream
+def _stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def _require_device(*ts):
+    dev = None
     for t in ts:
-        if t is not None and not t.is_cuda:
+        if t is None or not torch.is_tensor(t):
+            continue
+        if not t.is_cuda:
             raise ValueError("gdeconv runs on ROCm devices only: move tensors to 'cuda' "
                              "(the reference CPU path is not part of this engine)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"all tensors must be on one device (got {dev} and {t.device})")
+    return dev
+
+
+@contextlib.contextmanager
+def _on(device):
+    """Make ``device`` current for the duration of one engine call (the C side picks its internal
+    pipeline streams by the current HIP device)."""
+    with torch.cuda.device(device):
+        yield
 
 
 def _img(t, name):
@@ -29,10 +52,13 @@ def _img(t, name):
     return t.float().contiguous()
 
 
-def _galaxy_scalar(t, N, name):
-    """(tensor, stride) for a per-galaxy scalar given as [N,1,1,1], [N] or a 1-element tensor."""
+def _galaxy_scalar(t, N, name, device=None):
+    """(tensor, stride) for a per-galaxy scalar given as [N,1,1,1], [N], a 1-element tensor or a
+    Python number (placed on ``device``, the call's device)."""
     if not torch.is_tensor(t):
-        t = torch.tensor([float(t)], device="cuda")
+        t = torch.tensor([float(t)], dtype=torch.float32, device=device if device is not None else "cuda")
+    elif device is not None and t.device != torch.device(device):
+        raise ValueError(f"{name} is on {t.device}, the inputs on {device}")
     t = t.float().contiguous().reshape(-1)
     if t.numel() == N:
         return t, 1
@@ -51,23 +77,15 @@ def _psf(k, N, H, name="psf"):
     return k, gstride
 
 
-_WS = {}
-
-
 def workspace(N, H, W, device):
-    """Per-device cached workspace of gd_workspace_bytes(N, H, W) bytes (grown on demand)."""
+    """Scratch of gd_workspace_bytes(N, H, W) bytes for ONE call, from torch's caching allocator on
+    the current stream of ``device`` (freed back to that stream's pool when the caller drops it, so
+    reuse is stream-ordered; nothing is shared across streams or threads)."""
     lib = _lib.load()
     if not lib.gd_supported_size(H, W):
         raise ValueError(f"unsupported image size {H}x{W} (supported: square 32,48,64,96,128,256)")
     nbytes = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
-    if nbytes == 0:
-        raise ValueError(f"unsupported image size {H}x{W} (supported: square 32,48,64,96,128,256)")
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
-    buf = _WS.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-        _WS[key] = buf
-    return buf
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
 def empty_otf(N, H, W, device):
@@ -80,96 +98,114 @@ def supported(H, W):
 
 def psf_to_otf_half(psf, N, H, W):
     """Half-spectrum OTF [N, W//2+1, H] of ``psf_to_otf`` (utils/utils_torch.py:79-92)."""
-    _require_device(psf)
+    dev = _require_device(psf)
     lib = _lib.load()
-    k, gs = _psf(psf, N, H)
-    otf = empty_otf(N, H, W, k.device)
-    ws = workspace(N, H, W, k.device)
-    _lib.check(lib.gd_psf_to_otf(k.data_ptr(), gs, k.shape[2], k.shape[3], N, H, W, otf.data_ptr(),
-                                 ws.data_ptr(), _stream()), "gd_psf_to_otf")
+    with _on(dev):
+        k, gs = _psf(psf, N, H)
+        otf = empty_otf(N, H, W, dev)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_psf_to_otf(k.data_ptr(), gs, k.shape[2], k.shape[3], N, H, W, otf.data_ptr(),
+                                     ws.data_ptr(), _stream(dev)), "gd_psf_to_otf")
     return otf
 
 
 def conv_half(otf_half, x, conj=False):
-    """``conv_fft_batch(H, x)`` (utils/utils_torch.py:46-50) with H given as a half-spectrum OTF."""
-    _require_device(otf_half, x)
+    """``conv_fft_batch(H, x)`` (utils/utils_torch.py:46-50) with H given as a half-spectrum OTF
+    complex64 [1|N, W//2+1, H]; a 1-galaxy H applies to every image, as the reference's
+    ``fftn(x) * H`` broadcasts a [1,1,H,W] H."""
+    dev = _require_device(x, otf_half)
     lib = _lib.load()
     x = _img(x, "x")
     N, _, H, W = x.shape
+    K = W // 2 + 1
+    if otf_half.dtype != torch.complex64:
+        raise ValueError(f"otf_half must be complex64, got {otf_half.dtype}")
+    if otf_half.dim() != 3 or tuple(otf_half.shape[1:]) != (K, H) or otf_half.shape[0] not in (1, N):
+        raise ValueError(f"otf_half must be [1|N={N}, {K}, {H}] for {H}x{W} images, got {tuple(otf_half.shape)}")
     otf_half = otf_half.contiguous()
-    out = torch.empty_like(x)
-    ws = workspace(N, H, W, x.device)
-    _lib.check(lib.gd_conv_fft_batch(otf_half.data_ptr(), int(conj), x.data_ptr(), out.data_ptr(), N, H, W,
-                                     ws.data_ptr(), _stream()), "gd_conv_fft_batch")
+    gstride = K * H if (otf_half.shape[0] == N and N > 1) else 0
+    with _on(dev):
+        out = torch.empty_like(x)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_conv_fft_batch_strided(otf_half.data_ptr(), gstride, int(conj), x.data_ptr(),
+                                                 out.data_ptr(), N, H, W, ws.data_ptr(), _stream(dev)),
+                   "gd_conv_fft_batch_strided")
     return out
 
 
 def rfft2_half(x):
     """Half spectrum of real images, complex64 [N, W//2+1, H] (transposed), unnormalised."""
-    _require_device(x)
+    dev = _require_device(x)
     lib = _lib.load()
     x = _img(x, "x")
     N, _, H, W = x.shape
     K = W // 2 + 1
-    spec = torch.empty(N, 2, K, H, dtype=torch.complex64, device=x.device)
-    _lib.check(lib.gd_rfft2(x.data_ptr(), spec.data_ptr(), N, H, W, _stream()), "gd_rfft2")
+    with _on(dev):
+        spec = torch.empty(N, 2, K, H, dtype=torch.complex64, device=dev)
+        _lib.check(lib.gd_rfft2(x.data_ptr(), spec.data_ptr(), N, H, W, _stream(dev)), "gd_rfft2")
     return spec[:, 0].contiguous()
 
 
 def irfft2_half(spec, H, W):
     """Inverse of ``rfft2_half`` (normalised by 1/(H W)), fp32 [N,1,H,W]."""
-    _require_device(spec)
+    dev = _require_device(spec)
     lib = _lib.load()
     N, K = spec.shape[0], W // 2 + 1
-    buf = torch.zeros(N, 2, K, H, dtype=torch.complex64, device=spec.device)
-    buf[:, 0] = spec
-    out = torch.empty(N, 1, H, W, dtype=torch.float32, device=spec.device)
-    _lib.check(lib.gd_irfft2(buf.data_ptr(), out.data_ptr(), N, H, W, _stream()), "gd_irfft2")
+    if spec.dtype != torch.complex64 or tuple(spec.shape[1:]) != (K, H):
+        raise ValueError(f"spec must be complex64 [N, {K}, {H}], got {spec.dtype} {tuple(spec.shape)}")
+    with _on(dev):
+        buf = torch.zeros(N, 2, K, H, dtype=torch.complex64, device=dev)
+        buf[:, 0] = spec
+        out = torch.empty(N, 1, H, W, dtype=torch.float32, device=dev)
+        _lib.check(lib.gd_irfft2(buf.data_ptr(), out.data_ptr(), N, H, W, _stream(dev)), "gd_irfft2")
     return out
 
 
 def wiener(y, psf, alpha):
     """models/Wiener.py:10-20 on the HIP engine."""
-    _require_device(y, psf, alpha)
+    dev = _require_device(y, psf, alpha)
     lib = _lib.load()
     y = _img(y, "y")
     N, _, H, W = y.shape
-    k, gs = _psf(psf, N, H)
-    al, al_s = _galaxy_scalar(alpha, N, "alpha")
-    out = torch.empty_like(y)
-    ws = workspace(N, H, W, y.device)
-    _lib.check(lib.gd_wiener(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
-                             out.data_ptr(), N, H, W, ws.data_ptr(), _stream()), "gd_wiener")
+    with _on(dev):
+        k, gs = _psf(psf, N, H)
+        al, al_s = _galaxy_scalar(alpha, N, "alpha", dev)
+        out = torch.empty_like(y)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_wiener(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
+                                 out.data_ptr(), N, H, W, ws.data_ptr(), _stream(dev)), "gd_wiener")
     return out
 
 
 def richardson_lucy(y, psf, n_iters):
     """models/Richard_Lucy.py:10-24 on the HIP engine."""
-    _require_device(y, psf)
+    dev = _require_device(y, psf)
     lib = _lib.load()
     y = _img(y, "y")
     N, _, H, W = y.shape
-    k, gs = _psf(psf, N, H)
-    out = torch.empty_like(y)
-    otf = empty_otf(N, H, W, y.device)
-    ws = workspace(N, H, W, y.device)
-    _lib.check(lib.gd_richardson_lucy(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], int(n_iters),
-                                      out.data_ptr(), N, H, W, otf.data_ptr(), ws.data_ptr(), _stream()),
-               "gd_richardson_lucy")
+    with _on(dev):
+        k, gs = _psf(psf, N, H)
+        out = torch.empty_like(y)
+        otf = empty_otf(N, H, W, dev)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_richardson_lucy(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], int(n_iters),
+                                          out.data_ptr(), N, H, W, otf.data_ptr(), ws.data_ptr(), _stream(dev)),
+                   "gd_richardson_lucy")
     return out
 
 
 def filter_power(filt):
     """|FFT2(filt)|^2 over the half spectrum, fp32 [N, W//2+1, H] (transposed like the OTF): the
     Tikhonov regulariser LtL of models/Tikhonet.py:26-27 from the placed filter image."""
-    _require_device(filt)
+    dev = _require_device(filt)
     lib = _lib.load()
     f = _img(filt, "filt")
     N, _, H, W = f.shape
-    out = torch.empty(N, W // 2 + 1, H, dtype=torch.float32, device=f.device)
-    ws = workspace(N, H, W, f.device)
-    _lib.check(lib.gd_filter_power(f.data_ptr(), out.data_ptr(), N, H, W, ws.data_ptr(), _stream()),
-               "gd_filter_power")
+    with _on(dev):
+        out = torch.empty(N, W // 2 + 1, H, dtype=torch.float32, device=dev)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_filter_power(f.data_ptr(), out.data_ptr(), N, H, W, ws.data_ptr(), _stream(dev)),
+                   "gd_filter_power")
     return out
 
 
@@ -178,46 +214,50 @@ def filter_power_taps(filt_img, device):
     Laplacian) by direct DFT in double on the device (gd_filter_power_taps).  The tap list of the
     constant image is extracted on the host (parameter setup, like weights)."""
     lib = _lib.load()
+    device = torch.device(device)
     img = filt_img.detach().reshape(filt_img.shape[-2], filt_img.shape[-1]).float().cpu()
     H, W = img.shape
     nz = torch.nonzero(img)
-    rc = nz.to(torch.int32).contiguous().to(device)
-    vals = img[nz[:, 0], nz[:, 1]].contiguous().to(device)
-    out = torch.empty(1, W // 2 + 1, H, dtype=torch.float32, device=device)
-    _lib.check(lib.gd_filter_power_taps(rc.data_ptr() if len(nz) else None, vals.data_ptr() if len(nz) else None,
-                                        int(len(nz)), out.data_ptr(), H, W, _stream()), "gd_filter_power_taps")
+    with _on(device):
+        rc = nz.to(torch.int32).contiguous().to(device)
+        vals = img[nz[:, 0], nz[:, 1]].contiguous().to(device)
+        out = torch.empty(1, W // 2 + 1, H, dtype=torch.float32, device=device)
+        _lib.check(lib.gd_filter_power_taps(rc.data_ptr() if len(nz) else None,
+                                            vals.data_ptr() if len(nz) else None, int(len(nz)), out.data_ptr(),
+                                            H, W, _stream(device)), "gd_filter_power_taps")
     return out
 
 
 def tikhonov(y, psf, alpha, lam, ltl=None):
     """models/Tikhonet.py:15-31 (Tikhonov.forward) on the HIP engine: Re IFFT2(conj(H) FFT2(y/alpha) /
     (|H|^2 + lam LtL)); ``ltl`` None = filter 'Identity', else a half-spectrum [1|N, W//2+1, H]."""
-    _require_device(y, psf, alpha, lam, ltl)
+    dev = _require_device(y, psf, alpha, lam, ltl)
     lib = _lib.load()
     y = _img(y, "y")
     N, _, H, W = y.shape
-    k, gs = _psf(psf, N, H)
-    al, al_s = _galaxy_scalar(alpha, N, "alpha")
-    lm, lm_s = _galaxy_scalar(lam.detach() if torch.is_tensor(lam) else lam, N, "lam")
-    lptr, lgs = None, 0
-    if ltl is not None:
-        K = W // 2 + 1
-        ltl = ltl.float().contiguous()
-        if ltl.shape[-2:] != (K, H) or ltl.numel() not in (K * H, N * K * H):
-            raise ValueError(f"ltl must be [1|N, {K}, {H}], got {tuple(ltl.shape)}")
-        lptr, lgs = ltl.data_ptr(), (0 if ltl.numel() == K * H else K * H)
-    out = torch.empty_like(y)
-    ws = workspace(N, H, W, y.device)
-    _lib.check(lib.gd_tikhonov(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
-                               lm.data_ptr(), lm_s, lptr, lgs, out.data_ptr(), N, H, W, ws.data_ptr(), _stream()),
-               "gd_tikhonov")
+    with _on(dev):
+        k, gs = _psf(psf, N, H)
+        al, al_s = _galaxy_scalar(alpha, N, "alpha", dev)
+        lm, lm_s = _galaxy_scalar(lam.detach() if torch.is_tensor(lam) else lam, N, "lam", dev)
+        lptr, lgs = None, 0
+        if ltl is not None:
+            K = W // 2 + 1
+            ltl = ltl.float().contiguous()
+            if ltl.shape[-2:] != (K, H) or ltl.numel() not in (K * H, N * K * H):
+                raise ValueError(f"ltl must be [1|N, {K}, {H}], got {tuple(ltl.shape)}")
+            lptr, lgs = ltl.data_ptr(), (0 if ltl.numel() == K * H else K * H)
+        out = torch.empty_like(y)
+        ws = workspace(N, H, W, dev)
+        _lib.check(lib.gd_tikhonov(y.data_ptr(), k.data_ptr(), gs, k.shape[2], k.shape[3], al.data_ptr(), al_s,
+                                   lm.data_ptr(), lm_s, lptr, lgs, out.data_ptr(), N, H, W, ws.data_ptr(),
+                                   _stream(dev)), "gd_tikhonov")
     return out
 
 
 def subnet_features(otf128, params):
     """SubNet conv features [N, 1024] from the 128x128 half-spectrum OTF of the PSFs
     (``k_subnet_features``; ``params`` packed as documented in include/gdeconv.h)."""
-    _require_device(otf128, params)
+    dev = _require_device(otf128, params)
     lib = _lib.load()
     N = otf128.shape[0]
     if tuple(otf128.shape[1:]) != (65, 128) or otf128.dtype != torch.complex64:
@@ -225,9 +265,10 @@ def subnet_features(otf128, params):
     if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
         raise ValueError("bad SubNet parameter pack")
     otf128 = otf128.contiguous()
-    feat = torch.empty(N, 1024, dtype=torch.float32, device=otf128.device)
-    _lib.check(lib.gd_subnet_features(otf128.data_ptr(), params.contiguous().data_ptr(), feat.data_ptr(), N,
-                                      _stream()), "gd_subnet_features")
+    with _on(dev):
+        feat = torch.empty(N, 1024, dtype=torch.float32, device=dev)
+        _lib.check(lib.gd_subnet_features(otf128.data_ptr(), params.contiguous().data_ptr(), feat.data_ptr(), N,
+                                          _stream(dev)), "gd_subnet_features")
     return feat
 
 
@@ -237,7 +278,7 @@ class GaussXState:
     Images and PSFs are H x W (the PSF is padded like the image, so it must have the image's size)."""
 
     def __init__(self, y, psf, alpha):
-        _require_device(y, psf, alpha)
+        self.dev = _require_device(y, psf, alpha)
         self.lib = _lib.load()
         self.y = _img(y, "y")
         self.N, _, self.H, self.W = self.y.shape
@@ -245,18 +286,20 @@ class GaussXState:
         if tuple(self.psf.shape[-2:]) != (self.H, self.W):
             raise ValueError("UnrolledADMMGaussian pads the PSF like the image: psf must be H x W "
                              "(pad_double(kernel) at models/unrolled_admm_gaussian.py:122)")
-        self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha")
         N1 = max(self.N, 1)
         nbytes = int(self.lib.gd_gx_state_bytes(N1, self.H, self.W))
         if nbytes == 0:
             raise ValueError(f"UnrolledADMMGaussian: unsupported image size {self.H}x{self.W} "
                              "(supported: square 32, 48, 64, 128)")
-        dev = self.y.device
-        self.state = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        self.ws = torch.empty(int(self.lib.gd_workspace_bytes(N1, 2 * self.H, 2 * self.W)), dtype=torch.uint8,
-                              device=dev)
-        self.spec_bytes = int(self.lib.gd_gx_spec_bytes(N1, self.H, self.W))
-        self.z0 = self._init()   # the state is valid from construction on
+        with _on(self.dev):
+            self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
+            self.state = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            self.spec_bytes = int(self.lib.gd_gx_spec_bytes(N1, self.H, self.W))
+            self.z0 = self._init()   # the state is valid from construction on
+
+    def _ws(self):
+        """Per-call scratch on the 2x padded grid (stream-ordered caching allocator)."""
+        return workspace(self.N, 2 * self.H, 2 * self.W, self.dev)
 
     def init(self):
         """z0 = init_l2(Y, Ht, HtH, alpha) (:111-115), computed with the state at construction."""
@@ -267,17 +310,18 @@ class GaussXState:
         k = self.psf
         _lib.check(self.lib.gd_gx_init(self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3],
                                        self.alpha.data_ptr(), self.alpha_s, self.N, self.H, self.W,
-                                       self.state.data_ptr(), z0.data_ptr(), self.ws.data_ptr(), _stream()),
-                   "gd_gx_init")
+                                       self.state.data_ptr(), z0.data_ptr(), self._ws().data_ptr(),
+                                       _stream(self.dev)), "gd_gx_init")
         return z0
 
     def rho(self, rho):
-        return _galaxy_scalar(rho.detach() if torch.is_tensor(rho) else rho, self.N, "rho")
+        return _galaxy_scalar(rho.detach() if torch.is_tensor(rho) else rho, self.N, "rho", self.dev)
 
     def x_update(self, z, u, rho, x_prev=None, rho_prev=None, zin=False, save=False):
         """x = XUpdateGaussian(Y, Ht, HtH, z, u, rho) (:85-93).  ``u`` None = 0.  ``x_prev`` given:
         u <- u + rho_prev (x_prev - z) in place first (the dual update :145 of the previous
         iteration).  Returns (x, rho x + u if zin, saved X spectrum if save)."""
+        _require_device(z, u, x_prev, self.y)
         z = _img(z, "z")
         r, rs = self.rho(rho)
         if x_prev is not None:
@@ -293,9 +337,11 @@ class GaussXState:
         zi = torch.empty_like(self.y) if zin else None
         xs = torch.empty(self.spec_bytes, dtype=torch.uint8, device=self.y.device) if save else None
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-        _lib.check(self.lib.gd_gx_xupdate(z.data_ptr(), ptr(u), ptr(x_prev), r.data_ptr(), rs, ptr(rp), rps,
-                                          x.data_ptr(), ptr(zi), ptr(xs), self.N, self.H, self.W,
-                                          self.state.data_ptr(), self.ws.data_ptr(), _stream()), "gd_gx_xupdate")
+        with _on(self.dev):
+            _lib.check(self.lib.gd_gx_xupdate(z.data_ptr(), ptr(u), ptr(x_prev), r.data_ptr(), rs, ptr(rp), rps,
+                                              x.data_ptr(), ptr(zi), ptr(xs), self.N, self.H, self.W,
+                                              self.state.data_ptr(), self._ws().data_ptr(), _stream(self.dev)),
+                       "gd_gx_xupdate")
         return x, zi, xs
 
     def x_backward(self, grad_x, z, rho, xs):
@@ -305,10 +351,11 @@ class GaussXState:
         r, rs = self.rho(rho)
         gz, gu = torch.empty_like(self.y), torch.empty_like(self.y)
         part = torch.empty(self.N, self.W + 1, dtype=torch.float32, device=self.y.device)
-        _lib.check(self.lib.gd_gx_xupdate_backward(g.data_ptr(), z.data_ptr(), r.data_ptr(), rs, xs.data_ptr(),
-                                                   gz.data_ptr(), gu.data_ptr(), part.data_ptr(), self.N, self.H,
-                                                   self.W, self.state.data_ptr(), self.ws.data_ptr(), _stream()),
-                   "gd_gx_xupdate_backward")
+        with _on(self.dev):
+            _lib.check(self.lib.gd_gx_xupdate_backward(g.data_ptr(), z.data_ptr(), r.data_ptr(), rs, xs.data_ptr(),
+                                                       gz.data_ptr(), gu.data_ptr(), part.data_ptr(), self.N, self.H,
+                                                       self.W, self.state.data_ptr(), self._ws().data_ptr(),
+                                                       _stream(self.dev)), "gd_gx_xupdate_backward")
         return gz, gu, part.sum(1)
 
 
@@ -346,24 +393,21 @@ class ADMMState:
     input (x + u1)."""
 
     def __init__(self, y, psf, alpha, llh):
-        _require_device(y, psf, alpha)
+        self.dev = _require_device(y, psf, alpha)
         self.lib = _lib.load()
         self.y = _img(y, "y")
         self.N, _, self.H, self.W = self.y.shape
         self.psf, self.psf_gs = _psf(psf, self.N, self.H)
-        self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha")
         if llh not in _lib.GD_LLH:
             raise ValueError("llh must be 'Gaussian' or 'Poisson'")
         self.llh = _lib.GD_LLH[llh]
-        dev = self.y.device
+        if not self.lib.gd_supported_size(self.H, self.W):
+            raise ValueError(f"unsupported image size {self.H}x{self.W} (supported: square 32,48,64,96,128,256)")
         nbytes = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W, self.llh))
-        workspace(self.N, self.H, self.W, dev)   # validates the size
-        # a private workspace: the Gaussian path keeps x0's spectra in it from init to iteration 0,
-        # so a denoiser that itself calls the engine cannot clobber it
-        self.ws = torch.empty(max(16, int(self.lib.gd_workspace_bytes(max(self.N, 1), self.H, self.W))),
-                              dtype=torch.uint8, device=dev)
-        self.state = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        self.zin = torch.empty_like(self.y)
+        with _on(self.dev):
+            self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
+            self.state = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            self.zin = torch.empty_like(self.y)
         self.iter = 0
 
     @property
@@ -378,11 +422,14 @@ class ADMMState:
     def init(self, rho2_first):
         """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; rho2_first = (tensor, stride)."""
         r2, r2s = rho2_first
+        _require_device(r2, self.y)
         k = self.psf
-        _lib.check(self.lib.gd_admm_init(
-            self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
-            self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.state.data_ptr(),
-            self.zin.data_ptr(), self.ws.data_ptr(), _stream()), "gd_admm_init")
+        with _on(self.dev):
+            ws = workspace(self.N, self.H, self.W, self.dev)
+            _lib.check(self.lib.gd_admm_init(
+                self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
+                self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.state.data_ptr(),
+                self.zin.data_ptr(), ws.data_ptr(), _stream(self.dev)), "gd_admm_init")
         self.iter = 0
 
     def step(self, z, rho1, rho2, rho2_next, out=None):
@@ -397,11 +444,14 @@ class ADMMState:
         r1, r1s = rho1
         r2, r2s = rho2
         rn, rns = (rho2_next if rho2_next is not None else (None, 0))
-        _lib.check(self.lib.gd_admm_iter(
-            self.y.data_ptr(), z.data_ptr(), dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s,
-            r1.data_ptr(), r1s, r2.data_ptr(), r2s, None if rn is None else rn.data_ptr(), rns, self.llh,
-            self.iter, int(last), self.N, self.H, self.W, self.state.data_ptr(), self.ws.data_ptr(),
-            _stream()), "gd_admm_iter")
+        _require_device(z, dst, r1, r2, rn, self.y)
+        with _on(self.dev):
+            ws = workspace(self.N, self.H, self.W, self.dev)
+            _lib.check(self.lib.gd_admm_iter(
+                self.y.data_ptr(), z.data_ptr(), dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s,
+                r1.data_ptr(), r1s, r2.data_ptr(), r2s, None if rn is None else rn.data_ptr(), rns, self.llh,
+                self.iter, int(last), self.N, self.H, self.W, self.state.data_ptr(), ws.data_ptr(),
+                _stream(self.dev)), "gd_admm_iter")
         self.iter += 1
         return dst
 

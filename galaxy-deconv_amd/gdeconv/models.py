@@ -16,15 +16,17 @@
 Differences from the reference, all deliberate: the device is taken from the input (the reference
 hard-codes ``cuda:0``, ``models/Unrolled_ADMM.py:178``), the OTF is computed on the device (the
 reference builds it on the CPU every forward, ``utils/utils_torch.py:81``), CPU tensors are
-rejected (no CPU path), and unsupported reference variants raise instead of misbehaving:
-``denoiser='XDenseUNet'`` (not on the hot path), ``PnP=False`` (the reference's l1 ``Z_Update``
-call uses an undefined ``lam``, ``:208``).
+rejected (no CPU path), unsupported reference variants raise instead of misbehaving
+(``PnP=False``: the reference's l1 ``Z_Update`` call uses an undefined ``lam``, ``:208``), and
+``Unrolled_ADMM`` is inference-only: its forward raises under autograd when a parameter requires
+grad (the engine writes through raw pointers, so no graph would reach ``self.Z`` / ``self.init``;
+the differentiable variant is ``UnrolledADMMGaussian``, whose X update has a HIP backward).
 """
 import torch
 import torch.nn as nn
 
 from . import engine
-from .nets import SubNet, XDenseUNet, ZUpdateResUNet
+from .nets import SubNet, XDenseUNet, ZUpdateResUNet, ZUpdateXDenseUNet
 
 
 def _rho_view(rho_iters, n, N):
@@ -43,8 +45,6 @@ def _rho_view(rho_iters, n, N):
 class Unrolled_ADMM(nn.Module):
     def __init__(self, n_iters=8, llh="Poisson", denoiser="ResUNet", PnP=True, subnet=True):
         super().__init__()
-        if denoiser != "ResUNet":
-            raise NotImplementedError("only denoiser='ResUNet' is on the accelerated path")
         if not PnP:
             raise NotImplementedError("PnP=False (l1 Z_Update) is broken in the reference (undefined lam)")
         if llh not in ("Poisson", "Gaussian"):
@@ -54,7 +54,8 @@ class Unrolled_ADMM(nn.Module):
         self.PnP = PnP
         self.subnet = subnet
         self.denoiser = denoiser
-        self.Z = ZUpdateResUNet()
+        # models/Unrolled_ADMM.py:163: the ResUNet for 'ResUNet', the XDenseUNet for anything else
+        self.Z = ZUpdateResUNet() if denoiser == "ResUNet" else ZUpdateXDenseUNet()
         if self.subnet:
             self.init = SubNet(self.n)
         else:
@@ -67,6 +68,10 @@ class Unrolled_ADMM(nn.Module):
         return self.rho1_iters, self.rho2_iters
 
     def forward(self, y, kernel, alpha):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "Unrolled_ADMM on the HIP engine is inference-only (wrap the call in torch.no_grad() or "
+                "freeze the parameters); train UnrolledADMMGaussian, whose X update has a HIP backward")
         N = y.shape[0]
         rho1_iters, rho2_iters = self.rhos(kernel, alpha)
         st = engine.ADMMState(y, kernel, alpha, self.llh)

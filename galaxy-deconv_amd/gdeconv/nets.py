@@ -119,6 +119,17 @@ class ZUpdateResUNet(nn.Module):
         return out
 
 
+class ZUpdateXDenseUNet(ZUpdateResUNet):
+    """Z step with the XDenseUNet denoiser: ``z = XDenseUNet(z.float())`` (``Z_Update_XDenseUNet``,
+    ``models/Unrolled_ADMM.py:142-151``, selected by ``denoiser != 'ResUNet'`` at :163).  Keys read
+    ``Z.net.*`` like the reference's; micro-batched like the ResUNet step."""
+
+    def __init__(self):
+        nn.Module.__init__(self)
+        self.net = XDenseUNet()
+        self.micro_batch = None
+
+
 def _fold_conv_bn(conv, bn):
     """Eval-mode BatchNorm folded into the preceding conv: W' = W s, b' = (b - mean) s + beta,
     s = gamma / sqrt(var + eps).  Same function as conv -> BN up to fp32 rounding; it removes the

@@ -61,9 +61,14 @@ size_t gd_otf_bytes(int N, int H, int W);
 int gd_psf_to_otf(const float* psf, long long psf_gstride, int h, int w, int N, int H, int W,
                   void* otf_half, void* ws, void* stream);
 
-/* out = Re IFFT2(FFT2(x) * H) (conj != 0: * conj(H)). */
+/* out = Re IFFT2(FFT2(x) * H) (conj != 0: * conj(H)); one OTF per galaxy. */
 int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out, int N, int H, int W,
                       void* ws, void* stream);
+/* The same with otf_gstride complex elements between galaxies' OTFs: (W/2+1)*H (one per galaxy) or 0
+ * (one OTF for the whole batch: the broadcast of the reference's fftn(x) * H with H [1,1,H,W],
+ * utils/utils_torch.py:46-50).  Any other stride: GD_ERR_ARG. */
+int gd_conv_fft_batch_strided(const void* otf_half, long long otf_gstride, int conj, const float* x, float* out,
+                              int N, int H, int W, void* ws, void* stream);
 
 /* Forward real 2D FFT into image slot 0 of a workspace-shaped buffer `spec`
  * (gd_workspace_bytes(N,H,W) bytes; spectrum = first N*(W/2+1)*H complex of each galaxy's slot 0,
@@ -76,8 +81,8 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
  * OTF (Poisson).  llh = GD_LLH_GAUSSIAN keeps the state in the SPECTRAL domain - |H|^2,
  * conj(H) F(max(y,0)/alpha), F(u1), conj(H) F(v - u2) - since every step of the Gaussian iteration is
  * linear: one forward and one inverse transform per iteration.  GD_LLH_POISSON (sqrt in the V step)
- * keeps the OTF and u1, v - u2 as images.  The Gaussian path also hands x0's spectra from
- * gd_admm_init to the first gd_admm_iter through `ws`: keep the same workspace, untouched, in between.
+ * keeps the OTF and u1, v - u2 as images.  Everything a later call needs is in `state`; `ws`
+ * (gd_workspace_bytes) is scratch for the duration of one call only.
  *
  * gd_admm_init: OTF, x0 = clamp(init_l2) -> zin (the first denoiser input, x0 + u1 with u1 = 0),
  *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].

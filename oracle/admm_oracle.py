@@ -224,7 +224,18 @@ def normwise_error(out, ref):
     return (out - ref).abs().amax(1) / ref.abs().amax(1).clamp_min(1e-300)
 
 
+def pixel_error_floored(out, ref, floor=1e-5):
+    """Per-galaxy max over pixels of |out - ref| / max(|ref|, floor * max|ref|): the per-pixel relative
+    error with a floor (north_star's "1e-5 rel fp32 per pixel").  Pixels where the
+    reference is ~0 are judged against floor * the galaxy's peak instead of their own magnitude.
+    Returns [N]."""
+    out = out.detach().double().cpu().reshape(out.shape[0], -1)
+    ref = ref.detach().double().cpu().reshape(ref.shape[0], -1)
+    den = torch.maximum(ref.abs(), floor * ref.abs().amax(1, keepdim=True)).clamp_min(1e-300)
+    return ((out - ref).abs() / den).amax(1)
+
+
 __all__ = ["psf_to_otf", "conv_fft_batch", "x_update", "v_update_poisson", "v_update_gaussian",
            "init_l2", "admm_forward", "wiener", "richardson_lucy", "tikhonov", "laplacian_kernel",
            "pad_double", "crop_half", "gx_spectra", "gx_init_l2", "gx_x_update", "gx_forward",
-           "normwise_error"]
+           "normwise_error", "pixel_error_floored"]

@@ -28,11 +28,27 @@ def test_subnet_false_parameters():
 def test_unsupported_variants_raise():
     from gdeconv.models import Unrolled_ADMM
     with pytest.raises(NotImplementedError):
-        Unrolled_ADMM(denoiser="XDenseUNet")
-    with pytest.raises(NotImplementedError):
         Unrolled_ADMM(PnP=False)
     with pytest.raises(ValueError):
         Unrolled_ADMM(llh="Laplace")
+
+
+def test_xdenseunet_denoiser_selected_like_the_reference():
+    """models/Unrolled_ADMM.py:163: ResUNet for 'ResUNet', XDenseUNet for any other name."""
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.nets import XDenseUNet, ResUNet
+    assert isinstance(Unrolled_ADMM(n_iters=1, denoiser="XDenseUNet").Z.net, XDenseUNet)
+    assert isinstance(Unrolled_ADMM(n_iters=1, denoiser="ResUNet").Z.net, ResUNet)
+
+
+def test_unrolled_admm_is_inference_only():
+    """Under autograd with trainable parameters the drop-in raises instead of silently returning an
+    output with no graph to self.Z / self.init (the engine writes through raw pointers)."""
+    from gdeconv.models import Unrolled_ADMM
+    m = Unrolled_ADMM(n_iters=1, llh="Gaussian")
+    x = torch.zeros(1, 1, 48, 48)
+    with pytest.raises(NotImplementedError, match="inference-only"):
+        m(x, torch.zeros(1, 1, 48, 48), torch.ones(1))
 
 
 def test_weights_deterministic_and_loadable():

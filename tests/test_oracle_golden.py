@@ -43,14 +43,14 @@ def test_admm256_identity_denoiser(llh):
     assert torch.equal(out, T(g[f"{llh}_out"]))
 
 
-def _denoiser_and_subnet(n):
-    from gdeconv.nets import SubNet, ZUpdateResUNet
+def _denoiser_and_subnet(n, denoiser="ResUNet"):
+    from gdeconv.nets import SubNet, ZUpdateResUNet, ZUpdateXDenseUNet
     from gdeconv.weights import make_state_dict
 
     class M(torch.nn.Module):
         def __init__(self):
             super().__init__()
-            self.Z = ZUpdateResUNet()
+            self.Z = ZUpdateResUNet() if denoiser == "ResUNet" else ZUpdateXDenseUNet()
             self.init = SubNet(n)
 
     m = M()
@@ -77,6 +77,31 @@ def test_admm48_full_model(llh, n):
         for k in ("v", "z"):
             assert torch.equal(torch.stack(trace[k]), T(g[f"{llh}_n{n}_{k}"]))
         assert torch.equal(torch.stack(trace["x"][1:]), T(g[f"{llh}_n{n}_x"]))
+
+
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+def test_admm48_xdenseunet_denoiser(llh):
+    """Unrolled_ADMM(denoiser='XDenseUNet') (models/Unrolled_ADMM.py:142-151, :163): the oracle + the
+    host-side XDenseUNet / SubNet mirrors reproduce the reference's output bit for bit
+    (tests/golden/make_golden_r02.py)."""
+    torch.set_num_threads(8)
+    g = golden("admm_xdense48.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    m = _denoiser_and_subnet(2, "XDenseUNet")
+    with torch.no_grad():
+        rho1, rho2 = m.init(psf, alpha)
+        out = O.admm_forward(obs, psf, alpha, rho1, rho2, llh, denoise=m.Z)
+    assert torch.equal(out, T(g[f"{llh}_out"]))
+
+
+def test_xdenseunet_admm_state_dict_keys():
+    """The drop-in Unrolled_ADMM(denoiser='XDenseUNet') has the reference model's keys and shapes."""
+    import json
+    from gdeconv.models import Unrolled_ADMM
+    ref = json.loads(bytes(golden("admm_xdense48.npz")["state_dict_keys"]).decode())
+    m = Unrolled_ADMM(n_iters=2, llh="Gaussian", denoiser="XDenseUNet")
+    mine = {k: list(v.shape) for k, v in m.state_dict().items()}
+    assert mine == ref
 
 
 @pytest.mark.parametrize("tag", ["48", "256"])

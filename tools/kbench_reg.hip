@@ -201,5 +201,52 @@ int main(int argc, char** argv) {
         printf("  %-26s %7.2f\n", "whole workgroup", tot);
     }
 #endif
+    // the fused init (k_psf_rows<STATE> must have run: PSF compact rows in the U1 slot)
+    {
+        float* psf;
+        const int h = 48;
+        CK(hipMalloc(&psf, (size_t)N * h * h * 4));
+        hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, psf, (size_t)N * h * h, 5u, 0.f, 1e-3f);
+        Args b = t.a;
+        b.y = t.z; b.psf = psf; b.psf_gstride = h * h; b.h = h; b.o2 = t.zin;
+        const int bpg = (h / 2 + Geo<L>::LPB - 1) / Geo<L>::LPB;
+        auto rows = [&] { hipLaunchKernelGGL((k_psf_rows<L, true>), dim3(N * bpg), dim3(256), 0, 0, b); };
+        const float mr = time_ms(rows, reps);
+        const float mi = time_ms([&] { rows(); hipLaunchKernelGGL((k_gal_reg_init<L>), dim3(N), dim3(512), 0, 0, b); }, reps);
+        CK(hipGetLastError());
+        const double gi = N * (2 * img_b + 2.5 * half_b + 2.0 * h * K * 8) / 1e9;
+        printf("k_psf_rows<STATE> N=%d  %.3f ms; + k_gal_reg_init %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", N, mr, mi, gi / mi, gi);
+#if GD_FUSED_TRACE
+        const char* inames[] = {"start -> y loaded", "row FFTs", "A gather + park", "A: Y, OTF cols, update, IFFT",
+                                "B gather", "B: Y, OTF cols, update, IFFT", "I half 0", "I half 1 (+ x0 row FFTs)",
+                                "W: A gather + park", "W: A cols -> F(x0)", "W: B gather", "W: B cols -> F(x0)"};
+        const int order[] = {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12};
+        for (int n : {32, N}) {
+            b.N = n;
+            for (int v = 0; v < 2; ++v) {
+                CK(hipMemset(tr, 0, (size_t)N * 16 * 8));
+                rows();
+                hipLaunchKernelGGL((k_gal_reg_init<L>), dim3(n), dim3(512), 0, 0, b);
+                CK(hipDeviceSynchronize());
+            }
+            std::vector<unsigned long long> h2((size_t)n * 16);
+            CK(hipMemcpy(h2.data(), tr, h2.size() * 8, hipMemcpyDeviceToHost));
+            printf("init phase trace N=%d (mean us per workgroup):\n", n);
+            // stamps: 0 start, 1 y, 2..5 INIT slices (TB = 2), 6, 7 I halves, 8 I end, 9..12 W slices, 13 end
+            const int st[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
+            double tot = 0;
+            for (int k = 0; k < 13; ++k) {
+                double s = 0;
+                for (int i = 0; i < n; ++i) s += (double)(h2[i * 16 + st[k + 1]] - h2[i * 16 + st[k]]);
+                s = s / n / 100.0;
+                tot += s;
+                const char* nm = k == 8 ? "I end -> W" : inames[k < 8 ? k : k - 1];
+                printf("  %-30s %7.2f\n", nm, s);
+            }
+            printf("  %-30s %7.2f\n", "whole workgroup", tot);
+            (void)order;
+        }
+#endif
+    }
     return 0;
 }

@@ -29,6 +29,19 @@ MODE_NAMES = {
 def pretty(kname):
     if "k_subnet_features" in kname:
         return "k_subnet_features<128,FEATURES>"
+    m = re.search(r"k_gal_small_init<(\d+)>", kname)
+    if m:
+        return f"k_gal_small_init<{m.group(1)}>"
+    m = re.search(r"k_gal_small<(\d+), (true|false), (true|false)>", kname)
+    if m:
+        first, last = m.group(2) == "true", m.group(3) == "true"
+        return f"k_gal_small<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
+    m = re.search(r"k_gal_reg_init<(\d+)>", kname)
+    if m:
+        return f"k_gal_init<{m.group(1)},REG>"        # fused init, one launch (512 threads)
+    m = re.search(r"k_gal_reg<(\d+)>", kname)
+    if m:
+        return f"k_gal_reg<{m.group(1)}>"             # fused iteration (first / middle / last: runtime flags)
     m = re.search(r"(k_gal_iter2?)<(\d+), (true|false), (true|false)(?:, (\d+))?>", kname)
     if m:
         if m.group(5) == "1":
@@ -73,6 +86,10 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--iters", type=int, default=16,
                     help="ADMM iterations in the profiled run (bench --steps 1 --warmup 1: 2 x 8)")
+    ap.add_argument("--rl-calls", type=int, default=0,
+                    help="Richardson-Lucy workload: forwards in the profiled run (bench --steps 1 --warmup 1: 2); "
+                         "op_richardson_lucy<L> = every engine kernel's bytes / calls")
+    ap.add_argument("--n-iters", type=int, default=None, help="iterations per forward of the profiled workload")
     a = ap.parse_args()
     fetch, nf = per_launch(a.fetch, "FETCH_SIZE")
     write, _ = per_launch(a.write, "WRITE_SIZE")
@@ -92,7 +109,9 @@ def main():
     # whole Gaussian ADMM iteration (RF(z) -> C_G_ITER[0] -> RI(zin), all chunks): traffic per call
     L = a.size
     members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER_F>", f"k_col<{L},G_ITER_L>",
-               f"k_row_inv<{L},OUT1>", f"k_gal_iter<{L},MID>", f"k_gal_iter<{L},FIRST>", f"k_gal_iter<{L},LAST>"]
+               f"k_row_inv<{L},OUT1>", f"k_gal_iter<{L},MID>", f"k_gal_iter<{L},FIRST>", f"k_gal_iter<{L},LAST>",
+               f"k_gal_reg<{L}>", f"k_gal_small<{L},MID>", f"k_gal_small<{L},FIRST>", f"k_gal_small<{L},LAST>",
+               f"k_gal_small<{L},FIRST_LAST>"]
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in out["kernels"].items() if k in members)
     if tot:
         out["kernels"][f"op_admm_iter<{L},Gaussian>"] = {
@@ -102,11 +121,22 @@ def main():
     init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
     if f"k_gal_init<{L},ONE>" in out["kernels"]:
         init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},ONE>"]
+    if f"k_gal_init<{L},REG>" in out["kernels"]:
+        init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},REG>"]
+    if f"k_gal_small_init<{L}>" in out["kernels"]:
+        init = [f"k_gal_small_init<{L}>"]
     if all(k in out["kernels"] for k in init):
         out["kernels"][f"op_admm_init<{L},Gaussian>"] = {
             "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in init),
-            "launches": out["kernels"][init[1]]["launches"],
+            "launches": out["kernels"][init[-1]]["launches"],
             "note": "fused init: " + " + ".join(init) + ", per call"}
+    if a.rl_calls:
+        tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in out["kernels"].values())
+        out["kernels"][f"op_richardson_lucy<{L}>"] = {
+            "hbm_bytes_per_launch": tot / a.rl_calls, "launches": a.rl_calls,
+            "note": "every engine kernel of the Richardson-Lucy forward, per call"}
+    if a.n_iters is not None:
+        out["n_iters"] = a.n_iters
     json.dump(out, open(a.out, "w"), indent=1)
     for k, v in out["kernels"].items():
         if "read_bytes_per_launch" in v:
