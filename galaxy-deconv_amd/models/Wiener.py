@@ -1,2 +1,7 @@
 """Drop-in for reference ``models/Wiener.py``."""
 from gdeconv.models import Wiener  # noqa: F401
+
+
+def __getattr__(name):  # names this drop-in does not define come from the reference module
+    from gdeconv import refpath
+    return refpath.attr(__name__, name)

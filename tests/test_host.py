@@ -143,3 +143,48 @@ def test_denoiser_micro_batching_is_transparent():
     xf = x.clone().requires_grad_(True)
     z(xf).sum().backward()
     assert torch.allclose(xg.grad, xf.grad, rtol=0, atol=1e-6 * float(xf.grad.abs().max()))
+
+
+REFERENCE = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "models")), reason="reference checkout absent")
+def test_shims_fall_through_to_the_reference():
+    """With the drop-ins ahead of the reference on sys.path, the
+    reference's scripts still import: modules the shims do not provide resolve to the reference's
+    files (test.py:15 utils.utils_test, train.py:15 utils.utils_train), names a shim module does not
+    define come from the reference module (models.Unrolled_ADMM.X_Update, utils.utils_torch.conv_fft),
+    and the accelerated classes stay the drop-ins.  Runs in a subprocess, bytecode writing off (the
+    reference tree is read-only)."""
+    import subprocess
+    import sys
+    code = r'''
+import importlib.util, sys
+sys.dont_write_bytecode = True
+spec = importlib.util.find_spec("utils.utils_test")
+assert spec is not None and spec.origin.startswith("/root/reference/"), spec
+spec = importlib.util.find_spec("models.ADMMNet")
+assert spec is not None and spec.origin.startswith("/root/reference/"), spec
+import utils.utils_train as ut                       # imports utils.fit_ellipse from the reference
+assert ut.__file__.startswith("/root/reference/")
+from models.Unrolled_ADMM import Unrolled_ADMM, X_Update, Z_Update_XDenseUNet
+import gdeconv.models
+assert Unrolled_ADMM is gdeconv.models.Unrolled_ADMM
+assert X_Update.__module__ == "_gdref.models.Unrolled_ADMM", X_Update.__module__
+from utils.utils_torch import conv_fft_batch, conv_fft
+import gdeconv.spectral
+assert conv_fft_batch is gdeconv.spectral.conv_fft_batch and callable(conv_fft)
+try:
+    from models.Wiener import NoSuchName
+except ImportError:
+    pass
+else:
+    raise AssertionError("missing names must still raise")
+print("ok")
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(repo, "galaxy-deconv_amd"), REFERENCE]),
+               PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd="/tmp", capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
