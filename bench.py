@@ -257,14 +257,15 @@ def cpu_baseline(args):
 def main():
     args = parse()
     from gdeconv import _lib
-    from gdeconv.dist import init_process_group
+    from gdeconv.dist import init_process_group, local_device
     from gdeconv.synth import make_batch
 
     rank, world, local = init_process_group()
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = local_device(local)
+    torch.cuda.set_device(dev)
+    backend = dist.get_backend() if world > 1 else None
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     lib = _lib.load()
@@ -330,8 +331,9 @@ def main():
     elapsed = float(elapsed.item())
     gal_s = N * world * args.steps / elapsed
 
-    gather_ms = None
+    gather_ms, with_gather = None, None
     if world > 1:
+        # the optional final collection over xGMI (RCCL all_gather_into_tensor), timed on its own ...
         from gdeconv.dist import gather_batch
         torch.cuda.synchronize()
         dist.barrier()
@@ -339,6 +341,24 @@ def main():
         gather_batch(out, N * world)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        # ... and overlapped: step k's gather in flight (RCCL's stream) while step k + 1 computes
+        with torch.no_grad():
+            dist.barrier()
+            torch.cuda.synchronize()
+            tw = time.perf_counter()
+            pend = None
+            for _ in range(args.steps):
+                o_ = step()
+                if pend is not None:
+                    pend.wait()
+                pend = gather_batch(o_, N * world, async_op=True)
+            pend.wait()
+            torch.cuda.synchronize()
+            tw = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=dev)
+            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        with_gather = {"value": N * world * args.steps / float(tw.item()), "unit": "galaxies/s",
+                       "ms_per_step": float(tw.item()) * 1e3 / args.steps,
+                       "note": "each step's outputs all-gathered to every rank, overlapped with the next step"}
 
     # the same forward captured once as a hipGraph (gdeconv.graphs) and replayed: what a serving loop
     # pays once host launch overhead is gone (matters at 48^2; reported beside value, not as value)
@@ -467,7 +487,9 @@ def main():
         "data": "synthetic (gdeconv.synth, seeded); deterministic random weights (gdeconv.weights)",
         "config": {"workload": workload,
                    "global_batch": N * world, "image": [L, L], "psf": [48, 48], "n_iters": n,
-                   "llh": None if rl else args.llh, "parallelism": f"dp{world} (batch shards, no data-path collective)",
+                   "llh": None if rl else args.llh,
+                   "parallelism": f"dp{world} (batch shards, no data-path collective"
+                                  + (f"; {backend} process group, {world} ranks)" if backend else ")"),
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
@@ -489,6 +511,7 @@ def main():
     }
     if gather_ms is not None:
         rec["gather_ms"] = gather_ms
+        rec["with_gather"] = with_gather
     if graphed is not None:
         rec["graphed"] = graphed
     if ingest is not None:

@@ -1,6 +1,7 @@
 """World-size-2 gloo run of the N>1 host path on CPU: contiguous batch shards per rank, per-rank
-compute (the CPU oracle stands in for the per-GPU engine here), chunked all_gather of the
-outputs - reassembled result equals the single-process batch."""
+compute (the CPU oracle stands in for the per-GPU engine here), all_gather_into_tensor of the
+outputs (uneven / even shards, one collective or chunks, blocking or asynchronous) - the
+reassembled result equals the single-process batch."""
 import os
 import socket
 
@@ -32,10 +33,21 @@ def _worker(rank, world, port, q):
         obs, psf, alpha, _ = make_batch(N, 64, h=16, seed=4)  # every rank builds the same seeded batch
         a, b = shard_range(N, rank, world)
         local = O.wiener(obs[a:b], psf[a:b], alpha[a:b])
-        full = gather_batch(local, N, chunk_bytes=4096)  # force several chunks
+        full = gather_batch(local, N, chunk_bytes=4096)  # uneven shards, several chunks
+        ref = O.wiener(obs, psf, alpha)
+        ok = torch.equal(full, ref)
+        # even shards: one collective straight into the result, and chunked; asynchronous form
+        N2 = 6
+        o2, p2, a2, _ = make_batch(N2, 64, h=16, seed=5)
+        a, b = shard_range(N2, rank, world)
+        loc2 = O.wiener(o2[a:b], p2[a:b], a2[a:b])
+        ref2 = O.wiener(o2, p2, a2)
+        ok &= torch.equal(gather_batch(loc2, N2), ref2)
+        ok &= torch.equal(gather_batch(loc2, N2, chunk_bytes=4096), ref2)
+        pend = gather_batch(loc2, N2, chunk_bytes=3 * 64 * 64 * 4, async_op=True)
+        ok &= torch.equal(pend.wait(), ref2)
         if rank == 0:
-            ref = O.wiener(obs, psf, alpha)
-            q.put(bool(torch.equal(full, ref)))
+            q.put(bool(ok))
     finally:
         dist.destroy_process_group()
 
