@@ -89,6 +89,83 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
+// ---------------------------------------------------------------- packed complex (VOP3P)
+// The transforms compute on c2 = (re, im) in one aligned VGPR pair, so every complex add is one
+// v_pk_add_f32.  The products whose operands need their halves swapped or negated (a variable complex
+// multiply, multiplication by -+i inside an add) are written as single VOP3P instructions with op_sel /
+// neg modifiers: left to the compiler, the scalar form was re-paired by the SLP vectoriser with ~100
+// moves and sign xors per 256-point line (429 -> ~280 instructions per line FFT).
+typedef float c2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ c2 tc2(float2 a) { return c2{a.x, a.y}; }
+__device__ __forceinline__ float2 tf2(c2 a) { return make_float2(a.x, a.y); }
+// two halves of a * b / a * conj(b), issued separately so that independent products interleave (a VOP3P
+// result read by the next instruction costs an s_nop)
+__device__ __forceinline__ c2 pmul_t(c2 a, c2 b) {
+    c2 t;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(b));
+    return t;
+}
+template <bool CONJ>
+__device__ __forceinline__ c2 pmul_r(c2 a, c2 b, c2 t) {
+    c2 r;
+    if constexpr (CONJ)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    return r;
+}
+// a * b
+__device__ __forceinline__ c2 pmul(c2 a, c2 b) {
+    c2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(b));          // (ay by, ay bx)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[0,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    return r;                                                                                          // (ax bx - ay by, ax by + ay bx)
+}
+// a * conj(b)
+__device__ __forceinline__ c2 pmulc(c2 a, c2 b) {
+    c2 t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(b));          // (ay by, ay bx)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    return r;                                                                                          // (ax bx + ay by, ay bx - ax by)
+}
+// b + (-i) s (forward) / b + i s (inverse), one instruction
+#ifndef GD_FFT_ASM_MI
+#define GD_FFT_ASM_MI 1
+#endif
+template <bool INV>
+__device__ __forceinline__ c2 add_mi(c2 b, c2 s) {
+    if constexpr (!GD_FFT_ASM_MI) return INV ? b + c2{-s.y, s.x} : b + c2{s.y, -s.x};  // folded to op_sel / neg
+    c2 r;
+    if constexpr (INV)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(s));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(s));
+    return r;
+}
+// v * (re + i im) for compile-time constants (the compiler keeps (re, im) in an SGPR pair)
+__device__ __forceinline__ c2 cmul_const(c2 v, float re, float im) {
+    return __builtin_elementwise_fma(v.yy, c2{-im, re}, v.xx * c2{re, im});
+}
+template <bool INV>
+__device__ __forceinline__ c2 vmul_mi(c2 a) {
+    return INV ? c2{-a.y, a.x} : c2{a.y, -a.x};
+}
+template <int N, int M, bool INV>
+__device__ __forceinline__ c2 vtwmul(c2 v) {
+    constexpr int m = ((M % N) + N) % N;
+    if constexpr (m == 0) {
+        return v;
+    } else if constexpr (2 * m == N) {
+        return -v;
+    } else if constexpr (4 * m == N) {
+        return vmul_mi<INV>(v);
+    } else if constexpr (4 * m == 3 * N) {
+        return vmul_mi<!INV>(v);
+    } else {
+        return cmul_const(v, Twiddle<N, M, INV>::re, Twiddle<N, M, INV>::im);
+    }
+}
+
 // ---------------------------------------------------------------- in-register DFTs
 constexpr int first_factor(int n) { return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : 3); }
 
@@ -98,66 +175,73 @@ struct DFT {
     static constexpr int B = N / A;
     static_assert(A * B == N, "unsupported DFT size");
     // N = A*B, n = A*n2 + n1, k = k1 + B*k2
-    __device__ __forceinline__ static void run(float2 (&x)[N]) {
-        float2 t[A][B];
+    __device__ __forceinline__ static void run(c2 (&x)[N]) {
+        c2 t[A][B];
         static_for<0, A>([&](auto n1c) {
             constexpr int n1 = decltype(n1c)::value;
-            float2 y[B];
+            c2 y[B];
             static_for<0, B>([&](auto n2c) { y[decltype(n2c)::value] = x[A * decltype(n2c)::value + n1]; });
             DFT<B, INV>::run(y);
             static_for<0, B>([&](auto k1c) {
                 constexpr int k1 = decltype(k1c)::value;
-                t[n1][k1] = twmul<N, n1 * k1, INV>(y[k1]);
+                t[n1][k1] = vtwmul<N, n1 * k1, INV>(y[k1]);
             });
         });
         static_for<0, B>([&](auto k1c) {
             constexpr int k1 = decltype(k1c)::value;
-            float2 z[A];
+            c2 z[A];
             static_for<0, A>([&](auto n1c) { z[decltype(n1c)::value] = t[decltype(n1c)::value][k1]; });
             DFT<A, INV>::run(z);
             static_for<0, A>([&](auto k2c) { x[k1 + B * decltype(k2c)::value] = z[decltype(k2c)::value]; });
         });
     }
+    __device__ __forceinline__ static void run(float2 (&x)[N]) {
+        c2 v[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = tc2(x[i]);
+        run(v);
+#pragma unroll
+        for (int i = 0; i < N; ++i) x[i] = tf2(v[i]);
+    }
 };
 
 template <bool INV>
 struct DFT<1, INV> {
-    __device__ __forceinline__ static void run(float2 (&)[1]) {}
+    __device__ __forceinline__ static void run(c2 (&)[1]) {}
 };
 
 template <bool INV>
 struct DFT<2, INV> {
-    __device__ __forceinline__ static void run(float2 (&x)[2]) {
-        const float2 a = x[0], b = x[1];
-        x[0] = cadd(a, b);
-        x[1] = csub(a, b);
+    __device__ __forceinline__ static void run(c2 (&x)[2]) {
+        const c2 a = x[0], b = x[1];
+        x[0] = a + b;
+        x[1] = a - b;
     }
 };
 
 template <bool INV>
 struct DFT<3, INV> {
-    __device__ __forceinline__ static void run(float2 (&x)[3]) {
+    __device__ __forceinline__ static void run(c2 (&x)[3]) {
         constexpr float s3 = 0.866025403784438646763723170752936183f;  // sqrt(3)/2
-        const float2 t1 = cadd(x[1], x[2]);
-        const float2 t2 = make_float2(x[0].x - 0.5f * t1.x, x[0].y - 0.5f * t1.y);
-        const float2 d = csub(x[1], x[2]);
+        const c2 t1 = x[1] + x[2];
+        const c2 t2 = x[0] - 0.5f * t1;
+        const c2 d = s3 * (x[1] - x[2]);
         // forward: X1 = t2 - i s3 d ; X2 = t2 + i s3 d
-        const float2 e = mul_mi<INV>(cscale(d, s3));
-        x[0] = cadd(x[0], t1);
-        x[1] = cadd(t2, e);
-        x[2] = csub(t2, e);
+        x[0] = x[0] + t1;
+        x[1] = add_mi<INV>(t2, d);
+        x[2] = add_mi<!INV>(t2, d);
     }
 };
 
 template <bool INV>
 struct DFT<4, INV> {
-    __device__ __forceinline__ static void run(float2 (&x)[4]) {
-        const float2 a = cadd(x[0], x[2]), b = csub(x[0], x[2]);
-        const float2 c = cadd(x[1], x[3]), d = mul_mi<INV>(csub(x[1], x[3]));
-        x[0] = cadd(a, c);
-        x[2] = csub(a, c);
-        x[1] = cadd(b, d);
-        x[3] = csub(b, d);
+    __device__ __forceinline__ static void run(c2 (&x)[4]) {
+        const c2 a = x[0] + x[2], b = x[0] - x[2];
+        const c2 c = x[1] + x[3], d = x[1] - x[3];
+        x[0] = a + c;
+        x[2] = a - c;
+        x[1] = add_mi<INV>(b, d);
+        x[3] = add_mi<!INV>(b, d);
     }
 };
 
@@ -296,50 +380,82 @@ __device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2
     static_assert(F2 % F1 == 0, "line plan needs F1 | F2");
     static_assert(!LEAN || F2 == 16, "lean twiddles are for 16 points per lane");
     static_assert(!DPP || (F1 == 16 && F2 == 16), "register transpose is for 16 x 16 lines");
-    // stage A: DFT-F2 over n2 (lane j = n1), then twiddle W_L^{n1 k1}
-    DFT<F2, INV>::run(v);
-    if constexpr (LEAN) {
-        float2 t1[4], t4[4];
+    // stage A: DFT-F2 over n2 (lane j = n1), then twiddle W_L^{n1 k1} (the table holds the forward
+    // twiddles; the inverse multiplies by their conjugates)
+    if constexpr (DPP) {
+        DFT<F2, INV>::run(v);
+        if constexpr (LEAN) {
+            float2 t1[4], t4[4];
 #pragma unroll
-        for (int i = 1; i < 4; ++i) {
-            t1[i] = tw[j * i];
-            t4[i] = tw[4 * j * i];
-            if (INV) {
-                t1[i].y = -t1[i].y;
-                t4[i].y = -t4[i].y;
+            for (int i = 1; i < 4; ++i) {
+                t1[i] = tw[j * i];
+                t4[i] = tw[4 * j * i];
+                if (INV) {
+                    t1[i].y = -t1[i].y;
+                    t4[i].y = -t4[i].y;
+                }
+            }
+#pragma unroll
+            for (int k1 = 1; k1 < F2; ++k1) {
+                const int a = k1 & 3, b = k1 >> 2;
+                const float2 w = a == 0 ? t4[b] : (b == 0 ? t1[a] : cmul(t4[b], t1[a]));
+                v[k1] = cmul(v[k1], w);
+            }
+        } else {
+#pragma unroll
+            for (int k1 = 1; k1 < F2; ++k1) {
+                float2 w = tw[j * k1];
+                if (INV) w.y = -w.y;
+                v[k1] = cmul(v[k1], w);
             }
         }
-#pragma unroll
-        for (int k1 = 1; k1 < F2; ++k1) {
-            const int a = k1 & 3, b = k1 >> 2;
-            const float2 w = a == 0 ? t4[b] : (b == 0 ? t1[a] : cmul(t4[b], t1[a]));
-            v[k1] = cmul(v[k1], w);
-        }
-    } else {
-#pragma unroll
-        for (int k1 = 1; k1 < F2; ++k1) {
-            float2 w = tw[j * k1];  // j*k1 <= (F1-1)(F2-1) < L: no wrap
-            if (INV) w.y = -w.y;
-            v[k1] = cmul(v[k1], w);
-        }
-    }
-    if constexpr (DPP) {
         transpose16_dpp(v, j);  // lane j: v[n1] = (element k1 = j of lane n1)
         DFT<F1, INV>::run(v);   // lane j holds X[j + F1 k2] in v[k2]
         return;
     }
+    c2 x[F2];
 #pragma unroll
-    for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v[k1];
+    for (int i = 0; i < F2; ++i) x[i] = tc2(v[i]);
+    DFT<F2, INV>::run(x);
+    c2 w[F2], t[F2];
+    if constexpr (LEAN) {
+        c2 t1[4], t4[4];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+            t1[i] = tc2(tw[j * i]);
+            t4[i] = tc2(tw[4 * j * i]);
+        }
+        // W^{j (a + 4b)} = W^{4 j b} W^{j a}; the inverse multiplies by conj(t4 t1) = conj t4 conj t1
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            const int a = k1 & 3, b = k1 >> 2;
+            if (a != 0 && b != 0) t[k1] = pmul_t(t4[b], t1[a]);
+        }
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            const int a = k1 & 3, b = k1 >> 2;
+            w[k1] = a == 0 ? t4[b] : (b == 0 ? t1[a] : pmul_r<false>(t4[b], t1[a], t[k1]));
+        }
+    } else {
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) w[k1] = tc2(tw[j * k1]);  // j*k1 <= (F1-1)(F2-1) < L: no wrap
+    }
+#pragma unroll
+    for (int k1 = 1; k1 < F2; ++k1) t[k1] = pmul_t(x[k1], w[k1]);
+#pragma unroll
+    for (int k1 = 1; k1 < F2; ++k1) x[k1] = pmul_r<INV>(x[k1], w[k1], t[k1]);
+#pragma unroll
+    for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = tf2(x[k1]);
     wave_lds_sync();
     // stage B: lane j takes k1 = j + F1*m, all n1; DFT-F1 over n1
 #pragma unroll
     for (int mm = 0; mm < M; ++mm) {
-        float2 z[F1];
+        c2 z[F1];
 #pragma unroll
-        for (int n1 = 0; n1 < F1; ++n1) z[n1] = xch[n1 * LD + j + F1 * mm];
+        for (int n1 = 0; n1 < F1; ++n1) z[n1] = tc2(xch[n1 * LD + j + F1 * mm]);
         DFT<F1, INV>::run(z);
 #pragma unroll
-        for (int k2 = 0; k2 < F1; ++k2) v[mm + M * k2] = z[k2];
+        for (int k2 = 0; k2 < F1; ++k2) v[mm + M * k2] = tf2(z[k2]);
     }
     wave_lds_sync();  // the area may be rewritten by the next line_fft of this wave
 }
