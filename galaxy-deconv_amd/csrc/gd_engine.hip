@@ -484,7 +484,12 @@ template <int L>
 constexpr bool defer_w1() { return L == 256; }
 __device__ __forceinline__ float2 w1_value(float hh, float2 Gk, float2 Xk, float r2n) {
     const float d0 = 1.0f + r2n;
+#if GD_RCP_DIV
+    const float rd = __builtin_amdgcn_rcpf(d0);  // as gauss_math's 1/(1 + rho2'): per galaxy, not two divisions per bin
+    return make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) * rd, (r2n * (hh * Xk.y + 0.0f) + Gk.y) * rd);
+#else
     return make_float2((r2n * (hh * Xk.x + 0.0f) + Gk.x) / d0, (r2n * (hh * Xk.y + 0.0f) + Gk.y) / d0);
+#endif
 }
 
 struct GState {  // one bin's Gaussian state as loaded (U1 / G zero where the variant skips them)

@@ -433,7 +433,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 // One column of the init (NC = 1 per call): |H|^2, G -> state; C <- X0 / L^2
 template <int L>
 __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], const float2 (&Hc)[16], int g, int kx,
-                                             int j, float al) {
+                                             int j, float ial) {
     constexpr float inv_n = float(1.0 / double(L * L));
     j = opaque(j);
     kx = opaque(kx);
@@ -451,8 +451,8 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
             h4[e] = hh;
             g4[h][c] = Gk.x;
             g4[h][c + 1] = Gk.y;
-            const float lhs = hh + 1.0f / al;
-            C[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+            const float rl = __builtin_amdgcn_rcpf(hh + ial);  // lhs = HtH + 1/alpha; one reciprocal (1 ulp), not two divisions
+            C[s] = cscale(make_float2(Gk.x * rl, Gk.y * rl), inv_n);
         }
         *reinterpret_cast<f4v*>(a.s_hh + gb + soff_h(kx, q, j)) = h4;
 #pragma unroll
@@ -516,7 +516,9 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     const float al = a.alpha(g), r2n = a.rho2n(g);
     GD_TRACE(0);
 
-    // R: max(y, 0) / alpha (RF_YA)
+    // R: max(y, 0) / alpha (RF_YA), as a multiply by the galaxy's 1/alpha (within an ulp of the division;
+    // 128 IEEE divisions per lane were a third of this phase)
+    const float ial = 1.0f / al;
     float2 X[RG::PPL][F2];
     {
         const float* y = a.y + (size_t)g * L * L;
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         for (int q = 0; q < RG::PPL; ++q) {
             const float* r0 = y + (size_t)(2 * (line + LINES * q)) * L + j;
 #pragma unroll
-            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
+            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) * ial, fmaxf(r0[L + F1 * r], 0.f) * ial);
         }
     }
     __syncthreads();  // twiddles
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int u = 0; u < RG::CPL; ++u) {
                 float2 Hc[F2];
                 init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh);
-                init_update4<L>(a, CA[u], Hc, g, line + LINES * u, j, al);
+                init_update4<L>(a, CA[u], Hc, g, line + LINES * u, j, ial);
                 __builtin_amdgcn_sched_barrier(0);
             }
             lds_barrier();  // nyqc, nyqh complete
@@ -665,7 +667,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             if constexpr (INIT) {
                 float2 Hc[F2];
                 init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
-                init_update4<L>(a, CB[u], Hc, g, KS + line + LINES * u, j, al);
+                init_update4<L>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
             } else {
                 w1_update4<L>(a, CB[u], g, KS + line + LINES * u, j);
