@@ -296,6 +296,11 @@ def main():
     if rl:
         model, denoiser = RLForward(n).to(dev), None
         use_fused = False
+        fused_rl = lib.gd_set_fused_rl(1)
+        lib.gd_set_fused_rl(fused_rl)
+        rl_impl = ("fused, k_rl_reg (OTF, then each galaxy's whole loop in one 512-thread workgroup; x, y, OTF "
+                   "re-read from the Infinity Cache)" if (fused_rl and L == 256) else
+                   "whole RL loop per Infinity-Cache chunk (RIF/C chain)")
     else:
         model = build_model(n, args.llh, dev)
         denoiser = model.Z
@@ -493,8 +498,7 @@ def main():
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
-                                 if use_fused else ("whole RL loop per Infinity-Cache chunk (RIF/C chain)" if rl
-                                                    else "three-kernel")),
+                                 if use_fused else (rl_impl if rl else "three-kernel")),
                    "init": (None if rl else
                             ("fused, " + INIT_IMPL[fused_init] if fused_init else "chunked")
                             if (L == 256 and args.llh == "Gaussian") else

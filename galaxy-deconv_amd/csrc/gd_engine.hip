@@ -843,7 +843,7 @@ struct FusedGeo {
 
 // Column c of a slice from S = [pair][SLD] holding X_p[kx] at [c] and X_p[(L - kx) mod L] at [KS + c]:
 // row y's half spectrum R_y[kx] = (X + conj X')/2 (y even) or (X - conj X')/(2i) (y odd).
-template <int L>
+template <int L, int SLD = FusedGeo<L>::SLD>
 __device__ __forceinline__ void fused_gather(const float2* S, int c, int j, float2 (&C)[FusedGeo<L>::F2]) {
     using FG = FusedGeo<L>;
     c = opaque(c);
@@ -851,7 +851,7 @@ __device__ __forceinline__ void fused_gather(const float2* S, int c, int j, floa
 #pragma unroll
     for (int s = 0; s < FG::F2; ++s) {
         const int y = j + FG::F1 * s;
-        const float2 u = S[(y >> 1) * FG::SLD + c], v = S[(y >> 1) * FG::SLD + FG::KS + c];
+        const float2 u = S[(y >> 1) * SLD + c], v = S[(y >> 1) * SLD + FG::KS + c];
         C[s] = (y & 1) ? make_float2(0.5f * (u.y + v.y), 0.5f * (v.x - u.x))
                        : make_float2(0.5f * (u.x + v.x), 0.5f * (u.y - v.y));
     }
@@ -1577,6 +1577,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
 }
 
 #include "gd_galreg.hpp"  // k_gal_reg: the 512-thread, register-resident fused iteration
+#include "gd_rlreg.hpp"   // k_rl_reg: the whole Richardson-Lucy loop per galaxy on the same skeleton
 
 // Small-image helpers (L <= 128, spectra in LDS as D[kx][ky]):
 // a line's forward-FFT result (packed rows r, r+1) -> the two rows' half spectra, via the line's own
@@ -2142,6 +2143,11 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_reg");
     }
+    static int rl_reg(const Args& a, int n_iters, hipStream_t st) {
+        ProfScope ps(nm("k_rl_reg", 0), st);
+        hipLaunchKernelGGL((k_rl_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a, n_iters);
+        return check_launch("k_rl_reg");
+    }
     static int gal_reg_init(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kGalInitName, 4), st);
         hipLaunchKernelGGL((k_gal_reg_init<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
@@ -2182,6 +2188,7 @@ size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations at 256^2: 1 = k_gal_reg, 2 = k_gal_iter2, 3 = k_gal_iter (parking); 0 = chunked
+int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per galaxy), 0 = chunked chain
 int g_fused_init = 1;  // Gaussian init at 256^2 (+ k_psf_rows<STATE>): 1 = k_gal_reg_init, 2 = k_gal_iter<KM = 1> +
                        // k_gal_w1, 3 = k_gal_iter<KM = 3>; 0 = chunked
 
@@ -2395,6 +2402,13 @@ struct Ops {
         return Lc::template col<C_POWER>(a, st);
     }
     static int richardson_lucy(Args a0, int n_iters, hipStream_t st0) {
+        if constexpr (has_fused<L>()) {
+            if (g_fused_rl && n_iters > 0) {
+                // the OTF (chunked psf_to_otf), then every galaxy's whole loop in one launch
+                GD_TRY(for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) { return psf_to_otf(a, st); }));
+                return Lc::rl_reg(a0, n_iters, st0);
+            }
+        }
         // a.o0 = x (output, also the iterate); otf kept in a.otf.  The whole iteration loop runs per
         // chunk, so x, y, the OTF and the chunk's spectra stay cache-resident across all n_iters.
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
@@ -2465,7 +2479,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r02.1"; }
+const char* gd_engine_rev(void) { return "r02.3"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2796,6 +2810,12 @@ int gd_set_pipeline_streams(int streams) {
 int gd_set_fused_init(int on) {
     const int old = g_fused_init;
     g_fused_init = (on >= 1 && on <= 3) ? on : 0;
+    return old;
+}
+
+int gd_set_fused_rl(int on) {
+    const int old = g_fused_rl;
+    g_fused_rl = on ? 1 : 0;
     return old;
 }
 

@@ -155,13 +155,19 @@ __device__ __forceinline__ void reg_fft(float2 (&v)[16], int j, float2* xch, con
 #endif
 }
 
+#ifndef GD_REG_SLD_PAD
+#define GD_REG_SLD_PAD 1
+#endif
 template <int L>
 struct RegGeo {
     static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1;
     static constexpr int THREADS = 512, LINES = THREADS / F1;  // 32 lines of 16 lanes
     static constexpr int NP = L / 2, PPL = NP / LINES;          // 128 row pairs, 4 per line
     static constexpr int KS = L / 4, CPL = KS / LINES;          // 64 columns per slice, 2 per line
-    static constexpr int SLD = FusedGeo<L>::SLD;                // slice layout [pair][SLD] (as k_gal_iter)
+    // slice layout [pair][SLD] (k_gal_iter's, one slot longer): an odd row stride puts the 16 rows a
+    // line writes in phase I (column results -> row half spectra) on 16 distinct bank pairs (SLD = 132
+    // put every fourth row on the same banks: 4-way conflicts on those stores)
+    static constexpr int SLD = FusedGeo<L>::SLD + GD_REG_SLD_PAD;
     static constexpr int XCH = xch_elems<L>();
     static constexpr int HPL = (NP / 2) / LINES;                // row pairs per line in a half of phase I
     static constexpr int U = cmax(NP * SLD, LINES * XCH);
@@ -173,7 +179,7 @@ struct RegGeo {
     static constexpr int PK = (U - XA) / THREADS;
     static constexpr int PXB = PK / PPL;
     static_assert(F1 == 16 && F2 == 16 && PPL == 4 && CPL == 2 && HPL == 2, "256 x 256 geometry");
-    static_assert(SLD == 2 * KS + 4 && SLD > L / 2, "row half spectra fit a slice row");
+    static_assert(SLD >= 2 * KS && SLD > L / 2, "row half spectra fit a slice row");
     static_assert(PK >= F2 && PXB >= 1 && RB0 + PXB <= RB1, "parking area above the exchange areas");
 };
 
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     lds_barrier();
     float2 CA[RG::CPL][F2];  // columns line, line + LINES of slice A; later their results
 #pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CA[u]);
+    for (int u = 0; u < RG::CPL; ++u) fused_gather<L, SLD>(S, line + LINES * u, j, CA[u]);
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int y = j + F1 * s;
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     lds_barrier();
     float2 CB[RG::CPL][F2];
 #pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CB[u]);
+    for (int u = 0; u < RG::CPL; ++u) fused_gather<L, SLD>(S, line + LINES * u, j, CB[u]);
     lds_barrier();  // slice B read -> exchange areas + parked column A results (second column)
 #pragma unroll
     for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
@@ -562,7 +568,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         }
         lds_barrier();
 #pragma unroll
-        for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CA[u]);
+        for (int u = 0; u < RG::CPL; ++u) fused_gather<L, SLD>(S, line + LINES * u, j, CA[u]);
 #pragma unroll
         for (int s = 0; s < F2; ++s) {
             const int y = j + F1 * s;
@@ -649,7 +655,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         }
         lds_barrier();
 #pragma unroll
-        for (int u = 0; u < RG::CPL; ++u) fused_gather<L>(S, line + LINES * u, j, CB[u]);
+        for (int u = 0; u < RG::CPL; ++u) fused_gather<L, SLD>(S, line + LINES * u, j, CB[u]);
         lds_barrier();  // slice B read -> exchange areas (+ parked column A results)
         GD_TRACE(TB + 3);
         if constexpr (INIT) {

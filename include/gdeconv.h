@@ -174,6 +174,13 @@ int gd_set_pipeline_streams(int streams);
  * pass / row pass through the workspace).  Returns the previous setting; process-wide. */
 int gd_set_fused_iteration(int on);
 
+/* Richardson-Lucy at 256^2 (gd_richardson_lucy, models/Richard_Lucy.py:10-24): on = 1 (default) runs the
+ * OTF, then the whole n_iters loop of each galaxy inside one 512-thread workgroup (k_rl_reg: the
+ * galaxy's spectra stay on-chip; x, y and the OTF are re-read from the cache hierarchy); 0 selects the
+ * chunked chain (four launches per iteration through the workspace).  Returns the previous setting;
+ * process-wide. */
+int gd_set_fused_rl(int on);
+
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->

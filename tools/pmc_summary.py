@@ -39,6 +39,9 @@ def pretty(kname):
     m = re.search(r"k_gal_reg_init<(\d+)>", kname)
     if m:
         return f"k_gal_init<{m.group(1)},REG>"        # fused init, one launch (512 threads)
+    m = re.search(r"k_rl_reg<(\d+)>", kname)
+    if m:
+        return f"k_rl_reg<{m.group(1)}>"              # whole Richardson-Lucy loop per galaxy
     m = re.search(r"k_gal_reg<(\d+)>", kname)
     if m:
         return f"k_gal_reg<{m.group(1)}>"             # fused iteration (first / middle / last: runtime flags)
