@@ -2827,6 +2827,23 @@ int gd_set_fused_iteration(int on) {
 
 int gd_subnet_param_count(void) { return gd::subnet::kParams; }
 
+int gd_subnet_mlp_param_count(int n_out) {
+    return (n_out >= 1 && n_out <= gd::subnet::kMaxOut) ? gd::subnet::mlp_param_count(n_out) : 0;
+}
+
+int gd_subnet_rhos(const void* otf128_half, const float* params, const float* mlp_params, const float* alpha,
+                   long long alpha_stride, float* feat, float* rhos, int n_out, int N, void* stream) {
+    if (N < 0) return fail(GD_ERR_ARG, "negative batch");
+    if (n_out < 1 || n_out > gd::subnet::kMaxOut) return fail(GD_ERR_ARG, "n_out must be in [1, 64]");
+    if (N == 0) return GD_OK;
+    GD_TRY(gd_subnet_features(otf128_half, params, feat, N, stream));
+    ProfScope ps("k_subnet_mlp<128,0>", (hipStream_t)stream, 1);
+    hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((N + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
+                       dim3(gd::subnet::kMlpThreads), 0, (hipStream_t)stream, feat, mlp_params, alpha, alpha_stride,
+                       rhos, n_out, N);
+    return check_launch("k_subnet_mlp");
+}
+
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
     if (N == 0) return GD_OK;

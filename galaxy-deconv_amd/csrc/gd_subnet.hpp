@@ -129,14 +129,9 @@ __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, in
     return h.x * h.x + h.y * h.y;
 }
 
-__global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __restrict__ otf128,
-                                                             const float* __restrict__ params,
-                                                             float* __restrict__ feat, int N) {
-    __shared__ __attribute__((aligned(16))) float A[kRegionA];
-    __shared__ __attribute__((aligned(16))) float B[kRegionB];
-    const int g = blockIdx.x;
-    if (g >= N) return;  // uniform per block; no barrier crossed
-    const int tid = threadIdx.x;
+// The conv stack of galaxy g; the last layer writes the 1024 features to `out` (LDS or global).
+__device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, const float* __restrict__ params,
+                                           float* out, float* A, float* B, int g, int tid) {
     const float2* otf = otf128 + (size_t)g * 65 * 128;
     // Down(1,4): MaxPool2d(2) of |H|^2 (128x128) -> A[64][64]; pooled[i][j] = max |H|^2 over
     // rows ky = 2i, 2i+1 and columns kx = 2j, 2j+1.  Lanes take consecutive i (coalesced ky pairs).
@@ -160,7 +155,106 @@ __global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __re
     GD_SN_LAYER(6, 16, 16, 8, false, A, B)     // B[16][8][8]
 #undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
-    conv_layer<16, 16, 8, false>(B, feat + (size_t)g * 1024, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+    conv_layer<16, 16, 8, false>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+}
+
+__global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __restrict__ otf128,
+                                                             const float* __restrict__ params,
+                                                             float* __restrict__ feat, int N) {
+    __shared__ __attribute__((aligned(16))) float A[kRegionA];
+    __shared__ __attribute__((aligned(16))) float B[kRegionB];
+    const int g = blockIdx.x;
+    if (g >= N) return;  // uniform per block; no barrier crossed
+    conv_stack(otf128, params, feat + (size_t)g * 1024, A, B, g, threadIdx.x);
+}
+
+// ---- the SubNet's MLP (models/Unrolled_ADMM.py:68-74, :85-86) over a batch of feature vectors:
+//   h1 = ReLU(W1 [feat; alpha] + b1)  (1025 -> 64), h2 = ReLU(W2 h1 + b2)  (64 -> 64),
+//   out = Softplus(W3 h2 + b3) + 1e-6  (64 -> n_out)
+// kMlpG galaxies per 256-thread workgroup: thread (o, q) computes neuron o for galaxies q, q + 4, ...
+// reading the transposed weights (one coalesced 256-byte row per input for the whole wave) once per
+// workgroup - per galaxy a workgroup would re-read W1 (262 KB) through L2 for every galaxy.  fp32
+// FMAs in input order (a summation order of its own: within rounding of the GEMMs it replaces).
+// mlp: W1^T [1025][64] | b1 [64] | W2^T [64][64] | b2 [64] | W3^T [64][n_out] | b3 [n_out].
+constexpr int kHidden = 64, kFeat = 1024, kMaxOut = 64, kMlpG = 8, kMlpThreads = 512;
+constexpr int kMlpWaves = kMlpThreads / kHidden;  // layer 1: wave q sums inputs [q KQ, (q + 1) KQ)
+constexpr int kMlpKQ = kFeat / kMlpWaves;
+constexpr int mlp_param_count(int n_out) {
+    return (kFeat + 1) * kHidden + kHidden + kHidden * kHidden + kHidden + kHidden * n_out + n_out;
+}
+
+__global__ __launch_bounds__(kMlpThreads) void k_subnet_mlp(const float* __restrict__ feat,
+                                                           const float* __restrict__ mlp,
+                                                           const float* __restrict__ alpha, long long alpha_stride,
+                                                           float* __restrict__ rhos, int n_out, int N) {
+    static_assert(kMlpG == kMlpWaves, "layers 2, 3: one galaxy per wave");
+    __shared__ float X[kMlpG][kFeat + 1];
+    __shared__ float H[2][kMlpG][kHidden];
+    const int tid = threadIdx.x, g0 = blockIdx.x * kMlpG;
+    const int ng = N - g0 < kMlpG ? N - g0 : kMlpG;
+    for (int i = tid; i < kMlpG * kFeat; i += kMlpThreads) {
+        const int gg = i / kFeat, f = i - gg * kFeat;
+        X[gg][f] = gg < ng ? feat[(size_t)(g0 + gg) * kFeat + f] : 0.f;
+    }
+    if (tid < kMlpG) X[tid][kFeat] = tid < ng ? alpha[(long long)(g0 + tid) * alpha_stride] : 0.f;
+    __syncthreads();
+    const float* W1 = mlp;
+    const float* b1 = W1 + (kFeat + 1) * kHidden;
+    const float* W2 = b1 + kHidden;
+    const float* b2 = W2 + kHidden * kHidden;
+    const float* W3 = b2 + kHidden;
+    const float* b3 = W3 + kHidden * n_out;
+    const int o = tid % kHidden, q = tid / kHidden;  // q is wave-uniform
+    {
+        // layer 1: wave q sums inputs [KQ q, KQ q + KQ) (+ alpha, input 1024, for the last wave) for all
+        // the workgroup's galaxies (W1 read once per workgroup, 8 loads in flight per lane); then the
+        // waves' partial sums are added in a fixed order
+        float part[kMlpG];
+#pragma unroll
+        for (int gg = 0; gg < kMlpG; ++gg) part[gg] = 0.f;
+        const int i0 = q * kMlpKQ;
+        float wv[kMlpKQ];  // this lane's W1 column slice, all loads issued before the first FMA
+#pragma unroll
+        for (int k = 0; k < kMlpKQ; ++k) wv[k] = W1[(i0 + k) * kHidden + o];
+#pragma unroll
+        for (int k = 0; k < kMlpKQ; ++k) {
+#pragma unroll
+            for (int gg = 0; gg < kMlpG; ++gg) part[gg] = fmaf(wv[k], X[gg][i0 + k], part[gg]);
+        }
+        if (q == kMlpWaves - 1) {
+            const float w = W1[kFeat * kHidden + o];
+#pragma unroll
+            for (int gg = 0; gg < kMlpG; ++gg) part[gg] = fmaf(w, X[gg][kFeat], part[gg]);
+        }
+        float* P = &X[0][0];  // the inputs are consumed: partial sums [waves][G][64] reuse X
+        __syncthreads();
+#pragma unroll
+        for (int gg = 0; gg < kMlpG; ++gg) P[(q * kMlpG + gg) * kHidden + o] = part[gg];
+        __syncthreads();
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < kMlpWaves; ++w) v += P[(w * kMlpG + q) * kHidden + o];  // galaxy q
+        H[0][q][o] = fmaxf(v + b1[o], 0.f);
+    }
+    __syncthreads();
+    float acc = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < kHidden; ++i) acc = fmaf(W2[i * kHidden + o], H[0][q][i], acc);
+    H[1][q][o] = fmaxf(acc + b2[o], 0.f);
+    __syncthreads();
+    if (o < n_out) {
+        acc = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < kHidden; ++i) acc = fmaf(W3[i * n_out + o], H[1][q][i], acc);
+        {
+            const int gg = q;
+            if (gg < ng) {
+                const float v = acc + b3[o];
+                // nn.Softplus(beta = 1, threshold = 20), then + 1e-6 (:86)
+                rhos[(size_t)(g0 + gg) * n_out + o] = (v > 20.f ? v : log1pf(expf(v))) + 1e-6f;
+            }
+        }
+    }
 }
 
 }  // namespace subnet

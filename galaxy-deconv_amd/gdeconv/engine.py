@@ -254,6 +254,32 @@ def tikhonov(y, psf, alpha, lam, ltl=None):
     return out
 
 
+def subnet_rhos(otf128, params, mlp_params, alpha, n_out):
+    """The whole SubNet forward (``k_subnet_features`` + the batched ``k_subnet_mlp``: MLP, Softplus,
+    + 1e-6) -> [N, n_out]; ``mlp_params`` packed (transposed weights) as documented in include/gdeconv.h,
+    ``alpha`` [N] or one value."""
+    dev = _require_device(otf128, params, mlp_params, alpha)
+    lib = _lib.load()
+    N = otf128.shape[0]
+    if tuple(otf128.shape[1:]) != (65, 128) or otf128.dtype != torch.complex64:
+        raise ValueError("otf128 must be complex64 [N, 65, 128]")
+    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+        raise ValueError("bad SubNet parameter pack")
+    if mlp_params.numel() != lib.gd_subnet_mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
+        raise ValueError("bad SubNet MLP parameter pack")
+    al = alpha.reshape(-1).float().contiguous()
+    if al.numel() not in (1, N):
+        raise ValueError("alpha must hold 1 or N values")
+    otf128 = otf128.contiguous()
+    with _on(dev):
+        out = torch.empty(N, int(n_out), dtype=torch.float32, device=dev)
+        feat = torch.empty(N, 1024, dtype=torch.float32, device=dev)  # scratch (the features)
+        _lib.check(lib.gd_subnet_rhos(otf128.data_ptr(), params.contiguous().data_ptr(), mlp_params.contiguous().data_ptr(),
+                                      al.data_ptr(), 1 if al.numel() == N else 0, feat.data_ptr(), out.data_ptr(),
+                                      int(n_out), N, _stream(dev)), "gd_subnet_rhos")
+    return out
+
+
 def subnet_features(otf128, params):
     """SubNet conv features [N, 1024] from the 128x128 half-spectrum OTF of the PSFs
     (``k_subnet_features``; ``params`` packed as documented in include/gdeconv.h)."""
@@ -458,4 +484,4 @@ class ADMMState:
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
            "tikhonov", "filter_power", "filter_power_taps", "GaussXState", "gx_x_update",
-           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features"]
+           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos"]

@@ -212,6 +212,18 @@ class SubNet(nn.Module):
                 self._pack = (key, torch.cat(parts).float().contiguous())
         return self._pack[1]
 
+    def _packed_mlp(self):
+        """W1^T | b1 | W2^T | b2 | W3^T | b3 of the MLP (transposed nn.Linear weights) for gd_subnet_rhos."""
+        lin = [self.mlp[0], self.mlp[2], self.mlp[4]]
+        key = tuple((m.weight._version, m.bias._version, m.weight.data_ptr()) for m in lin)
+        if getattr(self, "_mpack", None) is None or self._mpack[0] != key:
+            with torch.no_grad():
+                parts = []
+                for m in lin:
+                    parts += [m.weight.t().reshape(-1), m.bias.reshape(-1)]
+                self._mpack = (key, torch.cat(parts).float().contiguous())
+        return self._mpack[1]
+
     def _double_convs(self):
         return [down.maxpool_conv[1] for down in self.conv_layers]
 
@@ -230,11 +242,20 @@ class SubNet(nn.Module):
     def forward(self, kernel, alpha):
         N, _, h, w = kernel.shape
         if self._engine_ok(kernel):
-            # HIP path: OTF at 128^2 (|.|^2 is shift invariant, so equal to |FFT2(pad128)|^2) and the
-            # fused conv stack k_subnet_features; the MLP below stays in PyTorch
+            # HIP path: OTF at 128^2 (|.|^2 is shift invariant, so equal to |FFT2(pad128)|^2), then the
+            # conv stack (k_subnet_features) and one batched MLP launch (k_subnet_mlp: MLP, Softplus, + 1e-6)
+            # (with autograd on and trainable MLP parameters - training UnrolledADMMGaussian, train.py:41 - the
+            # MLP stays in PyTorch after k_subnet_features so its parameters get gradients)
             from . import engine
             otf128 = engine.psf_to_otf_half(kernel, N, 128, 128)
-            feat = engine.subnet_features(otf128, self._packed_params().to(kernel.device))
+            dev = kernel.device
+            if not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
+                out = engine.subnet_rhos(otf128, self._packed_params().to(dev), self._packed_mlp().to(dev),
+                                         alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                if self.n_out == self.n:
+                    return out.view(N, 1, 1, self.n)
+                return out[:, :, 0:self.n].view(N, 1, 1, self.n), out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
+            feat = engine.subnet_features(otf128, self._packed_params().to(dev))
         else:
             h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
             w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2

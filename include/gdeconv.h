@@ -158,6 +158,16 @@ int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho
 int gd_subnet_param_count(void);
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream);
 
+/* The whole SubNet forward (models/Unrolled_ADMM.py:77-86): the features above into feat (caller
+ * scratch, [N][1024] floats), then one batched MLP launch [feat; alpha] -> 64 -> ReLU -> 64 -> ReLU ->
+ * n_out -> Softplus, + 1e-6 -> rhos [N][n_out] (rho1 = rhos[:, :n], rho2 = rhos[:, n:] for n_out = 2n).
+ * mlp_params: gd_subnet_mlp_param_count(n_out) floats, the nn.Linear weights TRANSPOSED: W1^T [1025][64] |
+ * b1 [64] | W2^T [64][64] | b2 [64] | W3^T [64][n_out] | b3 [n_out]; alpha: per-galaxy scalars with
+ * alpha_stride (0 = one alpha).  n_out in [1, 64]; gd_subnet_mlp_param_count returns 0 outside it. */
+int gd_subnet_mlp_param_count(int n_out);
+int gd_subnet_rhos(const void* otf128_half, const float* params, const float* mlp_params, const float* alpha,
+                   long long alpha_stride, float* feat, float* rhos, int n_out, int N, void* stream);
+
 /* Infinity-Cache pipelining: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
  * run over the batch in chunks of about `bytes` of workspace (default 96 MiB, i.e. 186 galaxies at
  * 256^2); consecutive chunks go to internal HIP streams (default 2) forked from and joined back into

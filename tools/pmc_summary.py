@@ -29,6 +29,8 @@ MODE_NAMES = {
 def pretty(kname):
     if "k_subnet_features" in kname:
         return "k_subnet_features<128,FEATURES>"
+    if "k_subnet_mlp" in kname:
+        return "k_subnet_mlp<128,MLP>"            # the SubNet's MLP, batched
     m = re.search(r"k_gal_small_init<(\d+)>", kname)
     if m:
         return f"k_gal_small_init<{m.group(1)}>"
