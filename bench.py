@@ -58,7 +58,7 @@ MODE_NAMES = {
               "G_INIT", "G_ITER", "G_W1", "G_ITER_F", "G_ITER_L", "G_ITER_FL"],
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
-    "k_subnet_features": ["FEATURES"],
+    "k_subnet_features": ["FEATURES", "PSF"],
     "k_subnet_mlp": ["MLP"],
     "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],

@@ -2844,6 +2844,26 @@ int gd_subnet_rhos(const void* otf128_half, const float* params, const float* ml
     return check_launch("k_subnet_mlp");
 }
 
+int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const float* params, const float* mlp_params,
+                       const float* alpha, long long alpha_stride, float* feat, float* rhos, int n_out, int N,
+                       void* stream) {
+    if (N < 0) return fail(GD_ERR_ARG, "negative batch");
+    if (n_out < 1 || n_out > gd::subnet::kMaxOut) return fail(GD_ERR_ARG, "n_out must be in [1, 64]");
+    if (h < 2 || h > gd::subnet::kPsfMaxH || (h & 1)) return fail(GD_ERR_UNSUPPORTED, "PSF side must be even and <= 64");
+    if (N == 0) return GD_OK;
+    {
+        ProfScope ps("k_subnet_features<128,1>", (hipStream_t)stream, 1);
+        hipLaunchKernelGGL(gd::subnet::k_subnet_features_psf, dim3(N), dim3(gd::subnet::kThreads), 0,
+                           (hipStream_t)stream, psf, psf_gstride, h, params, feat, N);
+        GD_TRY(check_launch("k_subnet_features_psf"));
+    }
+    ProfScope ps("k_subnet_mlp<128,0>", (hipStream_t)stream, 1);
+    hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((N + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
+                       dim3(gd::subnet::kMlpThreads), 0, (hipStream_t)stream, feat, mlp_params, alpha, alpha_stride,
+                       rhos, n_out, N);
+    return check_launch("k_subnet_mlp");
+}
+
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
     if (N == 0) return GD_OK;

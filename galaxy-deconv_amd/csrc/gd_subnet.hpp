@@ -130,6 +130,7 @@ __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, in
 }
 
 // The conv stack of galaxy g; the last layer writes the 1024 features to `out` (LDS or global).
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid);
 __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, const float* __restrict__ params,
                                            float* out, float* A, float* B, int g, int tid) {
     const float2* otf = otf128 + (size_t)g * 65 * 128;
@@ -142,6 +143,10 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
         A[i * 64 + j] = m;
     }
     __syncthreads();
+    conv_layers(params, out, A, B, tid);
+}
+// the four Down blocks from the pooled |H|^2 in A[64][64]
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
     const float* P = params;
 #define GD_SN_LAYER(l, CI, CO, S, POOL, IN, OUT)                                                   \
     conv_layer<CI, CO, S, POOL>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);           \
@@ -166,6 +171,118 @@ __global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __re
     const int g = blockIdx.x;
     if (g >= N) return;  // uniform per block; no barrier crossed
     conv_stack(otf128, params, feat + (size_t)g * 1024, A, B, g, threadIdx.x);
+}
+
+// ---- the same features straight from the PSF (h <= 64, even): |FFT2(pad128(psf))|^2 computed in the
+// workgroup (the separate OTF128 row / column launches and their 65 x 128 complex spectrum per galaxy
+// in HBM go away).  |FFT|^2 is invariant under circular shifts, so the PSF sits at the origin of the
+// 128 x 128 grid instead of F.pad's centred placement (:79-81).  Rows: 32 lines of 8 lanes transform
+// the packed row pairs (rows 2l + i 2l+1, zero beyond h); columns: 64 lines, line kx (< 64) one half-
+// spectrum column (its rows split out of the packed pairs), line 0 columns 0 and 64 (both real) packed;
+// |H|^2 of the 65 columns -> M [128][65], then MaxPool2 of the full map via Hermitian symmetry -> A.
+// LDS (float2 units of the 80 KiB A | B union): exchange areas [0, 64 x 136), packed row spectra
+// [4352, 8448), M (floats) [4096, 12416), twiddles [10112, 10240); the conv stack overwrites them all.
+constexpr int kPsfMaxH = 64;
+__device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, float* AB, int tid) {
+    constexpr int L = 128, F1 = 8, F2 = 16, XCH = F1 * (F2 + 1);
+    float2* S2 = reinterpret_cast<float2*>(AB);
+    float2* tw = S2 + 10112;
+    float2* Z = S2 + 4352;
+    float* M = AB + 4096;
+    fill_twiddles<L>(tw, tid, kThreads);
+    const int line = tid / F1, j = tid - line * F1;
+    __syncthreads();
+    if (line < kPsfMaxH / 2) {  // rows 2 line, 2 line + 1 (zero when >= h)
+        float2 v[F2];
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int c = j + F1 * r;
+            const bool in = 2 * line < h && c < h;
+            v[r] = in ? make_float2(psf[(2 * line) * h + c], psf[(2 * line + 1) * h + c]) : make_float2(0.f, 0.f);
+        }
+        line_fft<L, false>(v, j, S2 + line * XCH, tw);
+        __syncthreads();  // exchange areas -> packed spectra
+#pragma unroll
+        for (int r = 0; r < F2; ++r) Z[line * L + j + F1 * r] = v[r];
+    } else {
+        __syncthreads();
+    }
+    __syncthreads();
+    // column kx = line (line 0: 0 and 64 packed); row i = j + 8 r
+    float2 c[F2];
+    const int kx = line, km = (L - kx) & (L - 1);
+#pragma unroll
+    for (int r = 0; r < F2; ++r) {
+        const int i = j + F1 * r;
+        float2 val = make_float2(0.f, 0.f);
+        if (i < h) {
+            const float2* zp = Z + (i >> 1) * L;
+            if (line == 0) {
+                const float2 z0 = zp[0], z64 = zp[L / 2];
+                val = (i & 1) ? make_float2(z0.y, z64.y) : make_float2(z0.x, z64.x);
+            } else {
+                const float2 zk = zp[kx], zm = zp[km];
+                val = (i & 1) ? make_float2(0.5f * (zk.y + zm.y), 0.5f * (zm.x - zk.x))
+                              : make_float2(0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y));
+            }
+        }
+        c[r] = val;
+    }
+    __syncthreads();  // packed spectra read -> exchange areas
+    float2* my = S2 + line * XCH;
+    line_fft<L, false>(c, j, my, tw);
+    float m[F2], m64[F2];
+    if (line == 0) {  // split C0 + i C64 (both real columns) through the line's own exchange area
+#pragma unroll
+        for (int r = 0; r < F2; ++r) my[j + F1 * r] = c[r];
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < F2; ++r) {
+            const int ky = j + F1 * r;
+            const float2 z = c[r], zm = my[(L - ky) & (L - 1)];
+            const float2 c0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+            const float2 c64 = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+            m[r] = c0.x * c0.x + c0.y * c0.y;
+            m64[r] = c64.x * c64.x + c64.y * c64.y;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < F2; ++r) m[r] = c[r].x * c[r].x + c[r].y * c[r].y;
+    }
+    __syncthreads();  // exchange areas -> M
+#pragma unroll
+    for (int r = 0; r < F2; ++r) {
+        const int ky = j + F1 * r;
+        M[ky * 65 + kx] = m[r];
+        if (line == 0) M[ky * 65 + 64] = m64[r];
+    }
+    __syncthreads();
+    // MaxPool2d(2) of the full 128 x 128 |H|^2 -> A[64][64] (as k_subnet_features' first stage)
+    for (int p = tid; p < 64 * 64; p += kThreads) {
+        const int jj = p >> 6, ii = p & 63;
+        float mx = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            int ky = 2 * ii + (e & 1), kxx = 2 * jj + (e >> 1);
+            if (kxx > 64) {
+                kxx = 128 - kxx;
+                ky = (128 - ky) & 127;
+            }
+            mx = e == 0 ? M[ky * 65 + kxx] : fmaxf(mx, M[ky * 65 + kxx]);
+        }
+        AB[ii * 64 + jj] = mx;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads) void k_subnet_features_psf(const float* __restrict__ psf, long long psf_gstride,
+                                                                 int h, const float* __restrict__ params,
+                                                                 float* __restrict__ feat, int N) {
+    __shared__ __attribute__((aligned(16))) float AB[kRegionA + kRegionB];
+    const int g = blockIdx.x;
+    if (g >= N) return;  // uniform per block; no barrier crossed
+    psf_pool(psf + (long long)g * psf_gstride, h, AB, threadIdx.x);
+    conv_layers(params, feat + (size_t)g * 1024, AB, AB + kRegionA, threadIdx.x);
 }
 
 // ---- the SubNet's MLP (models/Unrolled_ADMM.py:68-74, :85-86) over a batch of feature vectors:

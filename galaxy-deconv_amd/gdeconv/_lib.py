@@ -57,6 +57,7 @@ SIGNATURES = {
     "gd_subnet_features": (_I, [_P, _P, _P, _I, _P]),
     "gd_subnet_mlp_param_count": (_I, [_I]),
     "gd_subnet_rhos": (_I, [_P, _P, _P, _P, _LL, _P, _P, _I, _I, _P]),
+    "gd_subnet_rhos_psf": (_I, [_P, _LL, _I, _P, _P, _P, _LL, _P, _P, _I, _I, _P]),
     "gd_profile_enable": (_I, [_I]),
     "gd_profile_collect": (_I, []),
     "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),

@@ -280,6 +280,33 @@ def subnet_rhos(otf128, params, mlp_params, alpha, n_out):
     return out
 
 
+def subnet_rhos_psf(psf, params, mlp_params, alpha, n_out):
+    """The whole SubNet forward from the PSFs (``k_subnet_features_psf``: |FFT2(pad128(psf))|^2 in the
+    kernel, then the conv stack; ``k_subnet_mlp``) -> [N, n_out]; PSF side even and <= 64."""
+    dev = _require_device(psf, params, mlp_params, alpha)
+    lib = _lib.load()
+    N = psf.shape[0]
+    k, gs = _psf(psf, N, 128)
+    h = k.shape[2]
+    if k.shape[3] != h or h % 2 or h > 64:
+        raise ValueError("subnet_rhos_psf needs an even square PSF of side <= 64")
+    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+        raise ValueError("bad SubNet parameter pack")
+    if mlp_params.numel() != lib.gd_subnet_mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
+        raise ValueError("bad SubNet MLP parameter pack")
+    al = alpha.reshape(-1).float().contiguous()
+    if al.numel() not in (1, N):
+        raise ValueError("alpha must hold 1 or N values")
+    with _on(dev):
+        out = torch.empty(N, int(n_out), dtype=torch.float32, device=dev)
+        feat = torch.empty(N, 1024, dtype=torch.float32, device=dev)  # scratch (the features)
+        _lib.check(lib.gd_subnet_rhos_psf(k.data_ptr(), gs, h, params.contiguous().data_ptr(),
+                                          mlp_params.contiguous().data_ptr(), al.data_ptr(), 1 if al.numel() == N else 0,
+                                          feat.data_ptr(), out.data_ptr(), int(n_out), N, _stream(dev)),
+                   "gd_subnet_rhos_psf")
+    return out
+
+
 def subnet_features(otf128, params):
     """SubNet conv features [N, 1024] from the 128x128 half-spectrum OTF of the PSFs
     (``k_subnet_features``; ``params`` packed as documented in include/gdeconv.h)."""
@@ -484,4 +511,4 @@ class ADMMState:
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
            "tikhonov", "filter_power", "filter_power_taps", "GaussXState", "gx_x_update",
-           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos"]
+           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos", "subnet_rhos_psf"]

@@ -247,15 +247,18 @@ class SubNet(nn.Module):
             # (with autograd on and trainable MLP parameters - training UnrolledADMMGaussian, train.py:41 - the
             # MLP stays in PyTorch after k_subnet_features so its parameters get gradients)
             from . import engine
-            otf128 = engine.psf_to_otf_half(kernel, N, 128, 128)
             dev = kernel.device
             if not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
-                out = engine.subnet_rhos(otf128, self._packed_params().to(dev), self._packed_mlp().to(dev),
-                                         alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                if h <= 64:  # |FFT2(pad128(psf))|^2 inside the feature kernel (no OTF128 pre-pass)
+                    out = engine.subnet_rhos_psf(kernel, self._packed_params().to(dev), self._packed_mlp().to(dev),
+                                                 alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                else:
+                    out = engine.subnet_rhos(engine.psf_to_otf_half(kernel, N, 128, 128), self._packed_params().to(dev),
+                                             self._packed_mlp().to(dev), alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
                 if self.n_out == self.n:
                     return out.view(N, 1, 1, self.n)
                 return out[:, :, 0:self.n].view(N, 1, 1, self.n), out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
-            feat = engine.subnet_features(otf128, self._packed_params().to(dev))
+            feat = engine.subnet_features(engine.psf_to_otf_half(kernel, N, 128, 128), self._packed_params().to(dev))
         else:
             h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
             w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2

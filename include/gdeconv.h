@@ -168,6 +168,13 @@ int gd_subnet_mlp_param_count(int n_out);
 int gd_subnet_rhos(const void* otf128_half, const float* params, const float* mlp_params, const float* alpha,
                    long long alpha_stride, float* feat, float* rhos, int n_out, int N, void* stream);
 
+/* gd_subnet_rhos from the PSFs themselves (psf [*][h][h], psf_gstride floats between galaxies, 0 = one
+ * shared PSF; h even, <= 64): |FFT2(pad128(psf))|^2 is computed inside the feature kernel, so no
+ * gd_psf_to_otf pre-pass and no 128^2 OTF buffer (models/Unrolled_ADMM.py:77-83). */
+int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const float* params, const float* mlp_params,
+                       const float* alpha, long long alpha_stride, float* feat, float* rhos, int n_out, int N,
+                       void* stream);
+
 /* Infinity-Cache pipelining: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
  * run over the batch in chunks of about `bytes` of workspace (default 96 MiB, i.e. 186 galaxies at
  * 256^2); consecutive chunks go to internal HIP streams (default 2) forked from and joined back into

@@ -448,6 +448,32 @@ def test_subnet_feature_kernel_matches_pytorch(dev):
     assert nerr(r2.reshape(64, -1).cpu(), r2_ref.reshape(64, -1).cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("h", [32, 48, 64])
+def test_subnet_rhos_from_psf_matches_otf_path(dev, h):
+    """k_subnet_features_psf (|FFT2(pad128(psf))|^2 in the kernel) + k_subnet_mlp against the OTF128
+    path (gd_psf_to_otf + k_subnet_features + k_subnet_mlp) and the PyTorch SubNet (fold off)."""
+    from gdeconv import engine
+    from gdeconv.nets import SubNet
+    from gdeconv.synth import make_batch
+    from gdeconv.weights import make_state_dict
+    net = SubNet(8)
+    net.load_state_dict(make_state_dict(net, 13))
+    net = net.to(dev).eval()
+    N = 21
+    _, psf, alpha, _ = make_batch(N, 64, h=h, seed=14 + h)
+    psf, alpha = psf.to(dev), alpha.to(dev)
+    with torch.no_grad():
+        p, m = net._packed_params().to(dev), net._packed_mlp().to(dev)
+        a = engine.subnet_rhos_psf(psf, p, m, alpha.reshape(-1), 16)
+        b = engine.subnet_rhos(engine.psf_to_otf_half(psf, N, 128, 128), p, m, alpha.reshape(-1), 16)
+        net.set_fold_bn(False)
+        r1_ref, r2_ref = net(psf, alpha)
+        net.set_fold_bn(True)
+    ref = torch.cat([r1_ref.reshape(N, -1), r2_ref.reshape(N, -1)], 1)
+    assert nerr(a.cpu(), b.cpu()) < 2e-6
+    assert nerr(a.cpu(), ref.cpu()) < 1e-5
+
+
 # ------------------------------------------------------------------ Infinity-Cache pipelining
 def test_pipelined_chunks_bit_identical(dev):
     """Chunked multi-stream execution (here 9 galaxies per chunk on 3 streams, incl. a ragged last

@@ -27,6 +27,8 @@ MODE_NAMES = {
 
 
 def pretty(kname):
+    if "k_subnet_features_psf" in kname:
+        return "k_subnet_features<128,PSF>"       # |FFT2(pad128(psf))|^2 in the kernel, then the conv stack
     if "k_subnet_features" in kname:
         return "k_subnet_features<128,FEATURES>"
     if "k_subnet_mlp" in kname:
