@@ -35,6 +35,31 @@ __device__ __forceinline__ void pin(float2 (&v)[N]) {
     for (int i = 0; i < N; i += 4) pin4(v[i], v[i + 1], v[i + 2], v[i + 3]);
 }
 
+// ---- Cache warming for the galaxy that will run next on this XCD.  Workgroups go to the XCDs round-robin
+// (block b -> XCD b mod 8 in practice; used for speed only), so galaxy g + 256 runs on g's XCD.  Phase I
+// of galaxy g issues LDS-DMA loads of that galaxy's rows (global_load_lds_dwordx4: 16 bytes per lane,
+// written into a 1 KiB sink nobody reads, no registers held), so its R phase finds them in the L2 /
+// Infinity Cache instead of waiting on HBM.  Ends with s_waitcnt vmcnt(0) before the workgroup exits.
+// Measured (profiles/r02m_warm.txt): the R phase's z wait 9.9 -> 5.7 us, but phase I grows 2 x 4.6 us
+// (the DMA issue and its traffic beside the zin stores): MID 1.642 -> 1.707 ms, init 1.41 -> 1.47 ms.
+// Off; kept as an experiment switch.
+#ifndef GD_REG_PF
+#define GD_REG_PF 0
+#endif
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* gbl_vptr;
+template <int L, int PART, int NPART>
+__device__ __forceinline__ void warm_next(const float* base, int g, int N, float4* sink, int tid, int nthreads) {
+    if (!GD_REG_PF) return;
+    const int gn = g + 256;
+    if (gn >= N) return;
+    const float4* src = reinterpret_cast<const float4*>(base + (size_t)gn * L * L);
+    constexpr int V4 = L * L / 4, PER = V4 / NPART;
+    for (int i = PART * PER + tid; i < (PART + 1) * PER; i += nthreads)
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(src + i), (lds_vptr)sink, 16, 0, 0);
+}
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ---- 16-byte state access.  At 256^2 the Gaussian state's bins inside a column are stored in the
 // order the column lines hold them, so a lane's bins are contiguous (gd_engine.hip: sidx_c / sidx_h,
 // used by every kernel that touches this state): lane j's bins ky = j + 16 s at 32 (s >> 1) + 2 j +
@@ -211,6 +236,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
     __shared__ float2 nyqx[L];      // line 0's split scratch (S is occupied)
     __shared__ float nyqo[L];       // x(., L/2)
+    __shared__ float4 pf_sink[64];  // warm_next's LDS-DMA target (never read)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
     const bool l0 = (line == 0);
@@ -384,6 +410,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
             }
         }
         for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        warm_next<L, hf, 2>(a.a0, g, a.N, pf_sink, tid, T);
         lds_barrier();
         float2 V[RG::HPL][F2];
 #pragma unroll
@@ -417,6 +444,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
             }
         }
     });
+    drain_vm();  // the LDS-DMA warm loads land before the workgroup (and its LDS) is gone
     __syncthreads();
     GD_TRACE(9);
 }
@@ -513,6 +541,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
     __shared__ float2 nyqh[L];      // the OTF's Nyquist column
     __shared__ float nyqo[L];       // x(., L/2)
+    __shared__ float4 pf_sink[64];  // warm_next's LDS-DMA target (never read)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
     const bool l0 = (line == 0);
@@ -705,6 +734,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             }
         }
         for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
+        warm_next<L, hf, 2>(a.y, g, a.N, pf_sink, tid, T);
         lds_barrier();
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
@@ -747,6 +777,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     // W: F(x0)'s columns -> W~ (no inverse)
     GD_TRACE(8);
     slices(std::false_type{});
+    drain_vm();  // the LDS-DMA warm loads land before the workgroup (and its LDS) is gone
     __syncthreads();
     GD_TRACE(13);
 }
