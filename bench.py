@@ -64,7 +64,9 @@ MODE_NAMES = {
     "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_reg": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_small": ["MID", "FIRST", "LAST", "FIRST_LAST"],
-    "k_gal_init": ["-", "Y", "W1", "ONE", "REG"],
+    "k_gal_init": ["-", "Y", "W1", "ONE", "REG", "POIS"],
+    "k_pois_a": ["MID", "FIRST", "LAST", "FIRST_LAST"],
+    "k_pois_b": ["ITER", "INIT"],
     "k_psf_rows": ["ROWS", "STATE"],
 }
 # fused Gaussian iteration / init implementations (gd_set_fused_iteration / gd_set_fused_init)
@@ -111,6 +113,14 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         rows = 2 * 2 * h * (L // 2 + 1) * 8 if L == 256 else 0  # k_psf_rows<STATE>'s compact rows, out and in
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
+        if fused and L == 256:
+            # two-pass (gd_poisreg.hpp): pass A z, |H|^2, U1, W~ in, U1, X, zin out (2 img + 4.5 half; first
+            # 3.5: no U1; last 2 img + 2.5 half: nothing but x written); pass B X, H, w, y in, w, W~ out
+            # (3 img + 3 half)
+            if n == 1:
+                return 2 * img + 1.5 * half
+            mid, first, last = 5 * img + 7.5 * half, 5 * img + 6.5 * half, 2 * img + 2.5 * half
+            return (first + mid * (n - 2) + last) / n
         # u1, w (= v - u2), z in; u1, w, zin out (+ y, the OTF half spectrum); the last iteration
         # reads z, u1, w, y, OTF and writes x only
         mid, last = 6 * img + 2 * half, 4 * img + half
@@ -283,6 +293,7 @@ def main():
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
     use_fused = bool(fused) and args.size in (32, 48, 64, 96, 128, 256) and args.llh == "Gaussian"
+    pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
     pipe_streams = lib.gd_set_pipeline_streams(0)
@@ -433,20 +444,20 @@ def main():
     kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
     pipelined = chunk_bytes > 0
     h_psf = psf.shape[-1]
-    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused, h_psf)}
+    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused or pois2, h_psf)}
     # every priced operation against the HBM spec (compulsory bytes / average call time)
     for k, (ms, c) in ops.items():
-        b = op_bytes(k, L, n, use_fused, h_psf)
+        b = op_bytes(k, L, n, use_fused or pois2, h_psf)
         if b:
             ach = b * N / (ms / c * 1e-3) / 1e9
             kernels[pretty(k)].update({"algorithmic_bytes_per_call": b * N, "achieved_GBs": ach,
                                        "frac_of_hbm_peak": ach / HBM_PEAK_GBS})
-    if (pipelined or use_fused) and priced_ops:
+    if (pipelined or use_fused or pois2) and priced_ops:
         # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
         # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
         dom_raw = max(priced_ops, key=lambda k: ops[k][0])
         dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
-        per_gal = op_bytes(dom_raw, L, n, use_fused, h_psf)
+        per_gal = op_bytes(dom_raw, L, n, use_fused or pois2, h_psf)
     else:
         priced = {k: v for k, v in kern.items() if kernel_bytes(k, L, n)} or kern
         dom_raw = max(priced, key=lambda k: kern[k][0])
@@ -499,10 +510,15 @@ def main():
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
-                                 if use_fused else (rl_impl if rl else "three-kernel")),
+                                 if use_fused else (rl_impl if rl else
+                                                    ("two whole-galaxy passes: k_gal_reg<POIS> (X update, u1, zin) + "
+                                                     "k_pois_b (Hx, V step, duals, conj(H) F(w))") if pois2
+                                                    else "three-kernel")),
                    "init": (None if rl else
                             ("fused, " + INIT_IMPL[fused_init] if fused_init else "chunked")
                             if (L == 256 and args.llh == "Gaussian") else
+                            (("k_psf_rows + k_gal_reg_init<POIS>" if fused_init else "chunked Gaussian chain")
+                             + " + k_pois_b<INIT>") if pois2 else
                             ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
                              else "chunked"))},
         "roofline": roofline,

@@ -37,6 +37,7 @@
 // v_{n+1} - u2_{n+1} is all the next X-update needs (algebraically identical to :207-213).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -84,6 +85,7 @@ struct Args {
     const float* ltl;      // Tikhonov |L|^2 half spectrum [*][K][L] (nullptr: filter 'Identity')
     long long ltl_gstride; // elements between galaxies' |L|^2 (0 = one shared filter)
     int otf_bcast;         // LOAD_OTF modes: one OTF for every galaxy (conv_fft_batch's broadcast H)
+    float2* s_x;           // Poisson two-pass at 256^2: X (pass A -> pass B), state layout as s_u1
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
@@ -680,7 +682,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             const float2 Gk = cmulc(P[s], Hk2);
             if (valid) {
                 a.s_hh[sflat_h<L>(ob + ky)] = hh;
-                a.s_g[sflat_c<L>(ob + ky)] = Gk;
+                a.s_g[sflat_c<L>(ob + ky)] = a.llh == GD_LLH_POISSON ? Hk2 : Gk;  // Poisson two-pass: the OTF
             }
             const float lhs = hh + 1.0f / al;
             P[s] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
@@ -969,11 +971,12 @@ __device__ __forceinline__ void unstash(const float2* my, float2 (&C)[FusedGeo<L
 // init_l2 (models/Unrolled_ADMM.py:170-175) per bin: |H|^2, G = conj(H) F(max(y,0)/alpha) kept as
 // state; returns X0 / L^2 = G / (|H|^2 + 1/alpha) / L^2 (the arithmetic of k_col<C_G_INIT>)
 template <int L>
-__device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, float2 Hk, float al, float inv_n) {
+__device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, float2 Hk, float al, float inv_n,
+                                           bool store_h = false) {
     const float hh = Hk.x * Hk.x + Hk.y * Hk.y;
     const float2 Gk = cmulc(Yk, Hk);
     a.s_hh[sflat_h<L>(o)] = hh;
-    a.s_g[sflat_c<L>(o)] = Gk;
+    a.s_g[sflat_c<L>(o)] = store_h ? Hk : Gk;  // Poisson (two-pass): the OTF itself in the G slot
     const float lhs = hh + 1.0f / al;
     return cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
 }
@@ -1578,6 +1581,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
 
 #include "gd_galreg.hpp"  // k_gal_reg: the 512-thread, register-resident fused iteration
 #include "gd_rlreg.hpp"   // k_rl_reg: the whole Richardson-Lucy loop per galaxy on the same skeleton
+#include "gd_poisreg.hpp" // k_pois_b: Poisson pass B (pass A is k_gal_reg<L, true>)
 
 // Small-image helpers (L <= 128, spectra in LDS as D[kx][ky]):
 // a line's forward-FFT result (packed rows r, r+1) -> the two rows' half spectra, via the line's own
@@ -2143,6 +2147,21 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_reg");
     }
+    static int pois_a(const Args& a, hipStream_t st) {
+        ProfScope ps(nm("k_pois_a", a.first + 2 * a.last), st);
+        hipLaunchKernelGGL((k_gal_reg<L, true>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_reg<POIS>");
+    }
+    static int pois_b(const Args& a, int init, hipStream_t st) {
+        ProfScope ps(nm("k_pois_b", init), st);
+        hipLaunchKernelGGL((k_pois_b<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a, init);
+        return check_launch("k_pois_b");
+    }
+    static int gal_reg_init_pois(const Args& a, hipStream_t st) {
+        ProfScope ps(nm(kGalInitName, 5), st);
+        hipLaunchKernelGGL((k_gal_reg_init<L, true>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
+        return check_launch("k_gal_reg_init<POIS>");
+    }
     static int rl_reg(const Args& a, int n_iters, hipStream_t st) {
         ProfScope ps(nm("k_rl_reg", 0), st);
         hipLaunchKernelGGL((k_rl_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a, n_iters);
@@ -2302,6 +2321,34 @@ struct Ops {
     static int irfft2(Args a, hipStream_t st) {
         GD_TRY(Lc::template col<C_INV>(a, st));
         return Lc::template ri<RI_OUT1>(a, st);
+    }
+    // Poisson in two whole-galaxy passes per iteration at 256^2 (gd_poisreg.hpp): the Gaussian init's
+    // |H|^2, x0 -> zin and F(x0) with the OTF in the G slot, then pass B with u2 = 0 (w1, W~1)
+    static int admm_init_pois2(Args a0, hipStream_t st0) {
+        if (g_fused_init && a0.h <= 64) {
+            GD_TRY(Lc::psf_rows_state(a0, st0));
+            GD_TRY(Lc::gal_reg_init_pois(a0, st0));
+        } else {
+            GD_TRY(for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
+                Args b = a;
+                GD_TRY(Lc::template rf<RF_YA>(b, st));
+                GD_TRY(Lc::psf_rows(b, st));
+                GD_TRY(Lc::template col<C_G_INIT>(b, st));  // llh = Poisson: stores H, not G
+                b.o0 = a.o2;
+                b.t_slot = 1;
+                GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
+                return Lc::template col<C_G_W1>(b, st);     // F(x0) -> the W~ slot (defer_w1)
+            }));
+        }
+        Args b = a0;
+        b.s_x = a0.s_w;  // X := F(x0)
+        return Lc::pois_b(b, 1, st0);
+    }
+    static int admm_iter_pois2(Args a, hipStream_t st0) {
+        // a.a0 = z, a.o0 = zin | out (pass A); a.o1 = w (pass B, in place)
+        GD_TRY(Lc::pois_a(a, st0));
+        if (a.last) return GD_OK;
+        return Lc::pois_b(a, 0, st0);
     }
     static int admm_init(Args a0, hipStream_t st0) {
         // Poisson: a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
@@ -2550,15 +2597,29 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
 size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
     if (!gd_supported_size(H, W) || N <= 0) return 0;
     const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
-    return llh == GD_LLH_GAUSSIAN ? spec / 2 + 3 * spec : spec + 2 * img;
+    if (llh == GD_LLH_GAUSSIAN) return spec / 2 + 3 * spec;
+    // Poisson: [otf | u1 | w] (three-kernel chain); at 256^2 also room for the two-pass layout
+    // [|H|^2 | H | U1 | W~ | X] + w (bind_state picks the layout from gd_set_fused_iteration)
+    return H == 256 ? std::max(spec + 2 * img, spec / 2 + 4 * spec + img) : spec + 2 * img;
 }
 
 namespace {
+bool pois_two_pass(int H, int llh) { return llh == GD_LLH_POISSON && H == 256 && g_fused != 0; }
 // state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral);
 // Poisson: [otf | u1 | w]
 void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H;
     float2* base = reinterpret_cast<float2*>(state);
+    if (pois_two_pass(H, llh)) {
+        a.s_hh = reinterpret_cast<float*>(base);
+        float2* c = base + spec / 2;
+        a.s_g = c;                 // the OTF H
+        a.s_u1 = c + spec;
+        a.s_w = c + 2 * spec;      // conj(H) F(w)
+        a.s_x = c + 3 * spec;      // X (pass A -> pass B)
+        a.o1 = reinterpret_cast<float*>(c + 4 * spec);  // w = v - u2 (spatial)
+        return;
+    }
     if (llh == GD_LLH_GAUSSIAN) {
         a.s_hh = reinterpret_cast<float*>(base);
         float2* c = base + spec / 2;  // spec is even (H even)
@@ -2591,6 +2652,7 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     ProfScope ps("op_admm_init<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN)
         return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
+    if (pois_two_pass(H, llh)) return Ops<256>::admm_init_pois2(a, (hipStream_t)stream);
     return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
 }
 
@@ -2617,6 +2679,11 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
         a.a0 = z;
         a.o0 = zin_or_out;
         return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter_gauss(a, (hipStream_t)stream); });
+    }
+    if (pois_two_pass(H, llh)) {
+        a.a0 = z;
+        a.o0 = zin_or_out;
+        return Ops<256>::admm_iter_pois2(a, (hipStream_t)stream);
     }
     // Poisson: spatial u1 / w (RF reads z, u1, w; RI writes u1, w and zin_or_out)
     a.a0 = z; a.a1 = a.o0; a.a2 = a.o1;

@@ -76,14 +76,41 @@ __device__ __forceinline__ void st4v(void* p, f4v v) {
 #endif
 }
 
+// Poisson pass A's bin (the X update and u1's dual, models/Unrolled_ADMM.py:209, :212, on spectra): W~
+// holds conj(H) F(w) with w = v - u2 (written by pass B), so X = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2
+// + rho2), U1' = (U1 + X) - Z; returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last); Xo = X
+// (pass B's input)
+__device__ __forceinline__ float2 pois_math(float hh, float2 U1, float2 Wt, float2 Zk, float r1, float r2, float inv_n,
+                                            float2& U1o, float2& Xo, bool last) {
+    const float lhs = r1 * hh + r2;
+    const float2 A = csub(Zk, U1);
+    const float rl = __builtin_amdgcn_rcpf(lhs);
+    const float2 X = make_float2((r1 * A.x + r2 * Wt.x) * rl, (r1 * A.y + r2 * Wt.y) * rl);
+    Xo = X;
+    if (last) return cscale(X, inv_n);
+    const float2 U1n = csub(cadd(U1, X), Zk);
+    U1o = U1n;
+    return cscale(cadd(X, U1n), inv_n);
+}
+
 // the Nyquist column, one bin per thread (ky = tid)
-template <int L>
+template <int L, bool POIS = false>
 __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float2 Zk, float r1, float r2, float r2n,
                                              bool first, bool last) {
     constexpr float inv_n = float(1.0 / double(L * L));
     const size_t cb = ((size_t)g * (L / 2 + 1) + L / 2) * L;
     const int pc = sidx_c<L>(ky);
     const float hh = a.s_hh[cb + sidx_h<L>(ky)];
+    if constexpr (POIS) {
+        const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
+        float2 U1n, Xo;
+        const float2 r = pois_math(hh, U1, a.s_w[cb + pc], Zk, r1, r2, inv_n, U1n, Xo, last);
+        if (!last) {
+            st_s(a.s_u1 + cb + pc, U1n);
+            st_s(a.s_x + cb + pc, Xo);
+        }
+        return r;
+    }
     const float2 Gk = (last && !first) ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
     const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
     float2 Wt = a.s_w[cb + pc];
@@ -106,19 +133,19 @@ __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float
 struct SGroup {
     f4v h, g[2], u[2], w[2];
 };
-template <int L>
+template <int L, bool POIS = false>
 __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb, int kx, int q, int j, bool first,
                                             bool last) {
     G.h = ld4v(a.s_hh + gb + soff_h(kx, q, j));
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const size_t off = gb + soff_c(kx, 2 * q + h, j);
-        G.g[h] = (last && !first) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);  // first: W~1 needs G
+        G.g[h] = (POIS || (last && !first)) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);  // first: W~1 needs G
         G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_u1 + off);
         G.w[h] = ld4v(a.s_w + off);
     }
 }
-template <int L, int NC, int D = GD_REG_DEPTH>
+template <int L, int NC, bool POIS = false, int D = GD_REG_DEPTH>
 __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16], int g, int kx0, int kstep, int j,
                                                float r1, float r2, float r2n, bool first, bool last) {
     constexpr float inv_n = float(1.0 / double(L * L));
@@ -129,7 +156,7 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
     const size_t gb = (size_t)g * (L / 2 + 1) * L;
     SGroup G[NG];
 #pragma unroll
-    for (int t = 0; t < D && t < NG; ++t) sgroup_load<L>(a, G[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
+    for (int t = 0; t < D && t < NG; ++t) sgroup_load<L, POIS>(a, G[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
@@ -141,9 +168,14 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
             float2 U1n, Wn;
             const float2 Gk = make_float2(G[t].g[h][c], G[t].g[h][c + 1]);
             float2 Wt = make_float2(G[t].w[h][c], G[t].w[h][c + 1]);
-            if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
-            C[u][4 * q + e] = gauss_math_rt(G[t].h[e], Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt,
-                                            C[u][4 * q + e], r1, r2, r2n, inv_n, U1n, Wn, last);
+            if constexpr (POIS) {  // Wn carries X (pass B's input)
+                C[u][4 * q + e] = pois_math(G[t].h[e], make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt, C[u][4 * q + e],
+                                            r1, r2, inv_n, U1n, Wn, last);
+            } else {
+                if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
+                C[u][4 * q + e] = gauss_math_rt(G[t].h[e], Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt,
+                                                C[u][4 * q + e], r1, r2, r2n, inv_n, U1n, Wn, last);
+            }
             uo[h][c] = U1n.x; uo[h][c + 1] = U1n.y;
             wo[h][c] = Wn.x; wo[h][c + 1] = Wn.y;
         }
@@ -152,10 +184,10 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
             for (int h = 0; h < 2; ++h) {
                 const size_t off = gb + soff_c(kx0 + kstep * u, 2 * q + h, j);
                 st4v(a.s_u1 + off, uo[h]);
-                st4v(a.s_w + off, wo[h]);
+                st4v((POIS ? a.s_x : a.s_w) + off, wo[h]);
             }
         }
-        if (t + D < NG) sgroup_load<L>(a, G[t + D], gb, kx0 + kstep * ((t + D) / 4), (t + D) % 4, j, first, last);
+        if (t + D < NG) sgroup_load<L, POIS>(a, G[t + D], gb, kx0 + kstep * ((t + D) / 4), (t + D) % 4, j, first, last);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -224,7 +256,9 @@ __device__ __forceinline__ void stagger_start(int g) {
 
 // First / last iteration as uniform runtime flags (a.first, a.last), not template variants: the MID
 // code's register allocation is spill-free, compile-time FIRST / LAST variants spilled 60-100 VGPRs.
-template <int L>
+// POIS: Poisson pass A (k_gal_reg<L, true>): the same skeleton with pois_math's update (no V step, no G;
+// U1', X out) and the last output x * alpha (models/Unrolled_ADMM.py:215)
+template <int L, bool POIS = false>
 __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     using RG = RegGeo<L>;
     constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
@@ -244,7 +278,8 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     fill_twiddles<L>(tw, tid, T);
     const float r1 = a.rho1(g), r2 = a.rho2(g);
     const bool first = __builtin_amdgcn_readfirstlane(a.first) != 0, last = __builtin_amdgcn_readfirstlane(a.last) != 0;
-    const float r2n = last ? 0.f : a.rho2n(g);
+    const float r2n = (POIS || last) ? 0.f : a.rho2n(g);
+    const float al = POIS ? a.alpha(g) : 1.f;
     stagger_start(g);
     GD_TRACE(0);
 
@@ -324,9 +359,9 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     }
     lds_barrier();  // nyqc complete
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
-        nyqc[tid] = gauss_bin4<L>(a, g, tid, nyqc[tid], r1, r2, r2n, first, last);
+        nyqc[tid] = gauss_bin4<L, POIS>(a, g, tid, nyqc[tid], r1, r2, r2n, first, last);
     }
-    fused_update4x<L, RG::CPL>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
+    fused_update4x<L, RG::CPL, POIS>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
     lds_barrier();  // Nyquist results
     GD_TRACE(4);
 #pragma unroll
@@ -382,7 +417,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         if (GD_REG_PINF) pin(CB[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
-    fused_update4x<L, RG::CPL>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last);
+    fused_update4x<L, RG::CPL, POIS>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CB[u], opaque(j), my, tw);
@@ -437,6 +472,12 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         for (int w = 0; w < RG::HPL; ++w) {
             reg_fft<L, true>(V[w], opaque(j), my, tw);
             float* o = out + (size_t)(hf * L / 2 + 2 * (line + LINES * w)) * L + j;
+            if constexpr (POIS) {
+                if (last) {  // x * alpha for Poisson (:215)
+#pragma unroll
+                    for (int r = 0; r < F2; ++r) V[w][r] = make_float2(V[w][r].x * al, V[w][r].y * al);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < F2; ++r) {
                 st_s(o + F1 * r, V[w][r].x);
@@ -465,7 +506,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 // complex).  No parking, 16-byte state accesses.
 
 // One column of the init (NC = 1 per call): |H|^2, G -> state; C <- X0 / L^2
-template <int L>
+template <int L, bool POIS = false>
 __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], const float2 (&Hc)[16], int g, int kx,
                                              int j, float ial) {
     constexpr float inv_n = float(1.0 / double(L * L));
@@ -483,8 +524,8 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
             const float hh = Hk.x * Hk.x + Hk.y * Hk.y;  // init_bin's arithmetic
             const float2 Gk = cmulc(C[s], Hk);
             h4[e] = hh;
-            g4[h][c] = Gk.x;
-            g4[h][c + 1] = Gk.y;
+            g4[h][c] = POIS ? Hk.x : Gk.x;  // Poisson two-pass: the OTF in the G slot (pass B needs H)
+            g4[h][c + 1] = POIS ? Hk.y : Gk.y;
             const float rl = __builtin_amdgcn_rcpf(hh + ial);  // lhs = HtH + 1/alpha; one reciprocal (1 ulp), not two divisions
             C[s] = cscale(make_float2(Gk.x * rl, Gk.y * rl), inv_n);
         }
@@ -529,7 +570,9 @@ __device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16],
     }
 }
 
-template <int L>
+// POIS: the Poisson two-pass init (k_gal_reg_init<L, true>): the same init_l2 and F(x0), but the OTF
+// itself goes to the G slot (the Poisson V step reads y, not G); pass B then forms w1 and W~1.
+template <int L, bool POIS = false>
 __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     using RG = RegGeo<L>;
     constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
@@ -634,12 +677,12 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int u = 0; u < RG::CPL; ++u) {
                 float2 Hc[F2];
                 init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh);
-                init_update4<L>(a, CA[u], Hc, g, line + LINES * u, j, ial);
+                init_update4<L, POIS>(a, CA[u], Hc, g, line + LINES * u, j, ial);
                 __builtin_amdgcn_sched_barrier(0);
             }
             lds_barrier();  // nyqc, nyqh complete
             if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-                nyqc[tid] = init_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], nyqh[tid], al, inv_n);
+                nyqc[tid] = init_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], nyqh[tid], al, inv_n, POIS);
             lds_barrier();  // Nyquist results
 #pragma unroll
             for (int s = 0; s < F2; ++s) {
@@ -702,7 +745,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             if constexpr (INIT) {
                 float2 Hc[F2];
                 init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
-                init_update4<L>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
+                init_update4<L, POIS>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
             } else {
                 w1_update4<L>(a, CB[u], g, KS + line + LINES * u, j);

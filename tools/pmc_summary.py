@@ -40,14 +40,19 @@ def pretty(kname):
     if m:
         first, last = m.group(2) == "true", m.group(3) == "true"
         return f"k_gal_small<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
-    m = re.search(r"k_gal_reg_init<(\d+)>", kname)
+    m = re.search(r"k_gal_reg_init<(\d+)(?:, (true|false))?>", kname)
     if m:
-        return f"k_gal_init<{m.group(1)},REG>"        # fused init, one launch (512 threads)
+        return f"k_gal_init<{m.group(1)},{'POIS' if m.group(2) == 'true' else 'REG'}>"  # fused init (512 threads)
+    m = re.search(r"k_pois_b<(\d+)>", kname)
+    if m:
+        return f"k_pois_b<{m.group(1)}>"              # Poisson pass B
     m = re.search(r"k_rl_reg<(\d+)>", kname)
     if m:
         return f"k_rl_reg<{m.group(1)}>"              # whole Richardson-Lucy loop per galaxy
-    m = re.search(r"k_gal_reg<(\d+)>", kname)
+    m = re.search(r"k_gal_reg<(\d+)(?:, (true|false))?>", kname)
     if m:
+        if m.group(2) == "true":
+            return f"k_pois_a<{m.group(1)}>"          # Poisson pass A
         return f"k_gal_reg<{m.group(1)}>"             # fused iteration (first / middle / last: runtime flags)
     m = re.search(r"(k_gal_iter2?)<(\d+), (true|false), (true|false)(?:, (\d+))?>", kname)
     if m:
@@ -125,6 +130,16 @@ def main():
             "hbm_bytes_per_launch": tot / a.iters, "launches": a.iters,
             "note": "sum over the iteration's RF/C/RI chunk launches; FETCH/WRITE_SIZE count L2<->fabric "
                     "traffic, Infinity-Cache hits included"}
+    pois = [f"k_pois_a<{L}>", f"k_pois_b<{L}>"]
+    if any(k in out["kernels"] for k in pois):  # Poisson two-pass: pass A (every iteration) + pass B (not the last)
+        ptot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in out["kernels"].items() if k in pois)
+        nb = out["kernels"].get(f"k_pois_b<{L}>", {}).get("launches", 0)
+        na = out["kernels"].get(f"k_pois_a<{L}>", {}).get("launches", 0)
+        # pass B's launches include the init's one per forward; a.iters = iterations in the run
+        init_b = max(0, nb - (na - na // max(1, a.n_iters or 8)))
+        out["kernels"][f"op_admm_iter<{L},Poisson>"] = {
+            "hbm_bytes_per_launch": (ptot - init_b * out["kernels"][f"k_pois_b<{L}>"]["hbm_bytes_per_launch"]) / a.iters,
+            "launches": a.iters, "note": "Poisson two-pass: pass A + pass B per call (the init's pass B excluded)"}
     init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
     if f"k_gal_init<{L},ONE>" in out["kernels"]:
         init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},ONE>"]
