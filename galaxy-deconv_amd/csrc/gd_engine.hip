@@ -86,6 +86,7 @@ struct Args {
     long long ltl_gstride; // elements between galaxies' |L|^2 (0 = one shared filter)
     int otf_bcast;         // LOAD_OTF modes: one OTF for every galaxy (conv_fft_batch's broadcast H)
     float2* s_x;           // Poisson two-pass at 256^2: X (pass A -> pass B), state layout as s_u1
+    int gH, gW;            // image rows / columns (the runtime-size path, gd_generic.hpp)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
@@ -1967,15 +1968,17 @@ __global__ __launch_bounds__((RowGeo<L, 1, RBX>::THREADS)) void k_row_invfwd(Arg
 // spectrum where |H|^2 is ~0, so its absolute error matters there; an fp32 FFT of the placed 3x3
 // stencil carries ~1e-6 absolute error, this carries none beyond the final rounding.
 __global__ __launch_bounds__(256) void k_sparse_power(const int* rc, const float* vals, int ntaps, float* out,
-                                                      int L, int K) {
+                                                      int H, int W, int K) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= K * L) return;
-    const int kx = idx / L, ky = idx - kx * L;
+    if (idx >= K * H) return;
+    const int kx = idx / H, ky = idx - kx * H;
+    const long long HW = (long long)H * W;
     double re = 0.0, im = 0.0;
     for (int t = 0; t < ntaps; ++t) {
-        const long long ph = ((long long)ky * rc[2 * t] + (long long)kx * rc[2 * t + 1]) % L;  // exact phase index
+        // phase ky r / H + kx c / W as an exact index modulo H W
+        const long long ph = ((long long)ky * rc[2 * t] * W + (long long)kx * rc[2 * t + 1] * H) % HW;
         double sn, cs;
-        sincospi(-2.0 * double(ph) / double(L), &sn, &cs);
+        sincospi(-2.0 * double(ph) / double(HW), &sn, &cs);
         re += double(vals[t]) * cs;
         im += double(vals[t]) * sn;
     }
@@ -2239,11 +2242,11 @@ inline PipeRes* pipe_res() {
 template <int L>
 constexpr bool has_fused() { return L == 256; }
 
-inline Args offset_args(const Args& a, int g0, int n, int L) {
+inline Args offset_args(const Args& a, int g0, int n, int H, int W) {
     Args b = a;
     b.N = n;
-    const size_t img = (size_t)g0 * L * L;
-    const size_t spec = (size_t)g0 * (L / 2 + 1) * L;
+    const size_t img = (size_t)g0 * H * W;
+    const size_t spec = (size_t)g0 * (W / 2 + 1) * H;
     if (b.otf && !b.otf_bcast) b.otf += spec;
     if (b.s_hh) b.s_hh += spec;
     if (b.s_g) b.s_g += spec;
@@ -2267,8 +2270,8 @@ inline Args offset_args(const Args& a, int g0, int n, int L) {
 
 // f(const Args& chunk, hipStream_t stream) enqueues one chunk's kernels on `stream`.
 template <typename F>
-int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
-    const size_t tgal = (size_t)2 * (L / 2 + 1) * L * sizeof(float2);  // workspace per galaxy
+int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
+    const size_t tgal = (size_t)2 * (W / 2 + 1) * H * sizeof(float2);  // workspace per galaxy
     int G = a.N;
     if (g_chunk_bytes) {
         const size_t g = g_chunk_bytes / tgal;
@@ -2287,8 +2290,8 @@ int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
     int rc = GD_OK;
     for (int g0 = 0, c = 0; g0 < a.N && rc == GD_OK; g0 += G, ++c) {
         const int n = (a.N - g0 < G) ? a.N - g0 : G;
-        Args b = offset_args(a, g0, n, L);
-        b.T = a.T + (size_t)(c % S) * G * 2 * (L / 2 + 1) * L;
+        Args b = offset_args(a, g0, n, H, W);
+        b.T = a.T + (size_t)(c % S) * G * 2 * (W / 2 + 1) * H;
         rc = f(b, S > 1 ? r->st[c % S] : st);
     }
     if (S > 1) {
@@ -2298,6 +2301,10 @@ int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
         }
     }
     return rc;
+}
+template <typename F>
+int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
+    return for_chunks_hw(a, L, L, st, std::forward<F>(f));
 }
 
 // Operation bodies, templated on L.
@@ -2476,39 +2483,55 @@ struct Ops {
     }
 };
 
-template <template <int> class OP, typename F>
-int dispatch(int L, F&& f) {
-    switch (L) {
-        case 32: return f(OP<32>{});
-        case 48: return f(OP<48>{});
-        case 64: return f(OP<64>{});
-        case 96: return f(OP<96>{});
-        case 128: return f(OP<128>{});
-        case 256: return f(OP<256>{});
-        default: return fail(GD_ERR_UNSUPPORTED, "unsupported image size (supported: 32, 48, 64, 96, 128, 256, square)");
+#include "gd_generic.hpp"  // GOps: the same operations for any other H x W (runtime-planned line FFTs)
+
+inline bool specialised_size(int H, int W) {
+    if (H != W) return false;
+    switch (H) {
+        case 32: case 48: case 64: case 96: case 128: case 256: return true;
+        default: return false;
     }
+}
+
+// Square 32/48/64/96/128/256 -> the compile-time-planned Ops<L>; any other H x W in [2, 1024]^2 -> GOps
+template <template <int> class OP, typename F>
+int dispatch(int H, int W, F&& f) {
+    if (H == W) {
+        switch (H) {
+            case 32: return f(OP<32>{});
+            case 48: return f(OP<48>{});
+            case 64: return f(OP<64>{});
+            case 96: return f(OP<96>{});
+            case 128: return f(OP<128>{});
+            case 256: return f(OP<256>{});
+            default: break;
+        }
+    }
+    if (gen::size_ok(H, W)) return f(GOps{});
+    return fail(GD_ERR_UNSUPPORTED, "unsupported image size (H and W must be in [2, 1024])");
 }
 
 inline int check_shape(int N, int H, int W) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
-    if (H != W) return fail(GD_ERR_UNSUPPORTED, "only square images are supported");
-    if (!gd_supported_size(H, W)) return fail(GD_ERR_UNSUPPORTED, "unsupported image size");
+    if (!specialised_size(H, W) && !gen::size_ok(H, W))
+        return fail(GD_ERR_UNSUPPORTED, "unsupported image size (H and W must be in [2, 1024])");
     return GD_OK;
 }
 
-inline int check_psf(int h, int w, int H) {
+inline int check_psf(int h, int w, int H, int W) {
     if (h != w) return fail(GD_ERR_ARG, "psf must be square (psf_to_otf uses ker.shape[2] for both axes)");
     if (h <= 0 || (h & 1)) return fail(GD_ERR_ARG, "psf side must be even (odd sizes fail in the reference's quadrant copy)");
-    if (h > H) return fail(GD_ERR_ARG, "psf larger than the image");
+    if (h > H || h > W) return fail(GD_ERR_ARG, "psf larger than the image");
     return GD_OK;
 }
 
-inline Args base_args(int N, void* ws, int L) {
+inline Args base_args(int N, void* ws, int H, int W) {
     Args a;
     std::memset(&a, 0, sizeof(a));
     a.N = N;
     a.T = reinterpret_cast<float2*>(ws);
-    (void)L;
+    a.gH = H;
+    a.gW = W;
     a.alpha = GalScalar{nullptr, 0};
     a.rho1 = a.rho2 = a.rho2n = a.alpha;
     return a;
@@ -2531,11 +2554,8 @@ const char* gd_engine_rev(void) { return "r02.4"; }
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
 int gd_supported_size(int H, int W) {
-    if (H != W) return 0;
-    switch (H) {
-        case 32: case 48: case 64: case 96: case 128: case 256: return 1;
-        default: return 0;
-    }
+    if (specialised_size(H, W)) return 1;   // compile-time-planned kernels
+    return gen::size_ok(H, W) ? 2 : 0;      // runtime-planned kernels (gd_generic.hpp)
 }
 
 size_t gd_workspace_bytes(int N, int H, int W) {
@@ -2552,12 +2572,12 @@ size_t gd_otf_bytes(int N, int H, int W) {
 int gd_psf_to_otf(const float* psf, long long psf_gstride, int h, int w, int N, int H, int W,
                   void* otf_half, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
-    GD_TRY(check_psf(h, w, H));
+    GD_TRY(check_psf(h, w, H, W));
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.otf = reinterpret_cast<float2*>(otf_half);
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::psf_to_otf(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::psf_to_otf(a, (hipStream_t)stream); });
 }
 
 int gd_conv_fft_batch(const void* otf_half, int conj, const float* x, float* out, int N, int H, int W,
@@ -2571,46 +2591,46 @@ int gd_conv_fft_batch_strided(const void* otf_half, long long otf_gstride, int c
     if (otf_gstride != 0 && otf_gstride != (long long)(W / 2 + 1) * H)
         return fail(GD_ERR_ARG, "otf_gstride must be 0 (one shared OTF) or (W/2+1)*H");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.otf = reinterpret_cast<float2*>(const_cast<void*>(otf_half));
     a.otf_bcast = otf_gstride == 0;
     a.a0 = x; a.o0 = out;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::conv(a, conj, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::conv(a, conj, (hipStream_t)stream); });
 }
 
 int gd_rfft2(const float* x, void* spec, int N, int H, int W, void* stream) {
     GD_TRY(check_shape(N, H, W));
     if (N == 0) return GD_OK;
-    Args a = base_args(N, spec, H);  // spectrum lives in image slot 0 of a T-shaped buffer
+    Args a = base_args(N, spec, H, W);  // spectrum lives in image slot 0 of a T-shaped buffer
     a.a0 = x;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::rfft2(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::rfft2(a, (hipStream_t)stream); });
 }
 
 int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
     GD_TRY(check_shape(N, H, W));
     if (N == 0) return GD_OK;
-    Args a = base_args(N, spec, H);
+    Args a = base_args(N, spec, H, W);
     a.o0 = x;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::irfft2(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::irfft2(a, (hipStream_t)stream); });
 }
 
 size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
     if (!gd_supported_size(H, W) || N <= 0) return 0;
     const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
-    if (llh == GD_LLH_GAUSSIAN) return spec / 2 + 3 * spec;
+    if (llh == GD_LLH_GAUSSIAN) return (spec / 8 + 1) / 2 * 8 + 3 * spec;  // |H|^2 padded to 8-byte alignment
     // Poisson: [otf | u1 | w] (three-kernel chain); at 256^2 also room for the two-pass layout
     // [|H|^2 | H | U1 | W~ | X] + w (bind_state picks the layout from gd_set_fused_iteration)
-    return H == 256 ? std::max(spec + 2 * img, spec / 2 + 4 * spec + img) : spec + 2 * img;
+    return (H == 256 && W == 256) ? std::max(spec + 2 * img, spec / 2 + 4 * spec + img) : spec + 2 * img;
 }
 
 namespace {
-bool pois_two_pass(int H, int llh) { return llh == GD_LLH_POISSON && H == 256 && g_fused != 0; }
+bool pois_two_pass(int H, int W, int llh) { return llh == GD_LLH_POISSON && H == 256 && W == 256 && g_fused != 0; }
 // state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral);
 // Poisson: [otf | u1 | w]
 void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H;
     float2* base = reinterpret_cast<float2*>(state);
-    if (pois_two_pass(H, llh)) {
+    if (pois_two_pass(H, W, llh)) {
         a.s_hh = reinterpret_cast<float*>(base);
         float2* c = base + spec / 2;
         a.s_g = c;                 // the OTF H
@@ -2622,7 +2642,7 @@ void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     }
     if (llh == GD_LLH_GAUSSIAN) {
         a.s_hh = reinterpret_cast<float*>(base);
-        float2* c = base + spec / 2;  // spec is even (H even)
+        float2* c = base + (spec + 1) / 2;  // |H|^2: spec floats, rounded up to whole float2
         a.s_g = c;
         a.s_u1 = c + spec;
         a.s_w = c + 2 * spec;
@@ -2639,10 +2659,10 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
                  int llh, int N, int H, int W, void* state, float* zin, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
-    GD_TRY(check_psf(h, w, H));
+    GD_TRY(check_psf(h, w, H, W));
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.alpha = GalScalar{alpha, alpha_stride};
     a.rho2n = GalScalar{rho2, rho2_stride};
@@ -2651,9 +2671,9 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     a.o2 = zin;
     ProfScope ps("op_admm_init<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN)
-        return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
-    if (pois_two_pass(H, llh)) return Ops<256>::admm_init_pois2(a, (hipStream_t)stream);
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
+        return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
+    if (pois_two_pass(H, W, llh)) return Ops<256>::admm_init_pois2(a, (hipStream_t)stream);
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
 }
 
 int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float* alpha, long long alpha_stride,
@@ -2664,7 +2684,7 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
     if (N == 0) return GD_OK;
     if (!last && rho2_next == nullptr) return fail(GD_ERR_ARG, "rho2_next required unless last");
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.y = y;
     bind_state(a, state, N, H, W, llh);
     a.alpha = GalScalar{alpha, alpha_stride};
@@ -2678,9 +2698,9 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     if (llh == GD_LLH_GAUSSIAN) {
         a.a0 = z;
         a.o0 = zin_or_out;
-        return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter_gauss(a, (hipStream_t)stream); });
+        return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_iter_gauss(a, (hipStream_t)stream); });
     }
-    if (pois_two_pass(H, llh)) {
+    if (pois_two_pass(H, W, llh)) {
         a.a0 = z;
         a.o0 = zin_or_out;
         return Ops<256>::admm_iter_pois2(a, (hipStream_t)stream);
@@ -2688,65 +2708,67 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     // Poisson: spatial u1 / w (RF reads z, u1, w; RI writes u1, w and zin_or_out)
     a.a0 = z; a.a1 = a.o0; a.a2 = a.o1;
     a.o2 = zin_or_out;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::admm_iter(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_iter(a, (hipStream_t)stream); });
 }
 
 int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
               long long alpha_stride, float* x, int N, int H, int W, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
-    GD_TRY(check_psf(h, w, H));
+    GD_TRY(check_psf(h, w, H, W));
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.alpha = GalScalar{alpha, alpha_stride};
     a.o0 = x;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::wiener(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::wiener(a, (hipStream_t)stream); });
 }
 
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
-    GD_TRY(check_psf(h, w, H));
+    GD_TRY(check_psf(h, w, H, W));
     if (n_iters < 0) return fail(GD_ERR_ARG, "n_iters must be >= 0");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.otf = reinterpret_cast<float2*>(otf_half);
     a.o0 = x;
     ProfScope ps("op_rl<" + std::to_string(H) + ",0>", (hipStream_t)stream, 1);
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::richardson_lucy(a, n_iters, (hipStream_t)stream); });
 }
 
 int gd_tikhonov(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
                 long long alpha_stride, const float* lam, long long lam_stride, const float* ltl,
                 long long ltl_gstride, float* x, int N, int H, int W, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
-    GD_TRY(check_psf(h, w, H));
+    GD_TRY(check_psf(h, w, H, W));
     if (lam == nullptr) return fail(GD_ERR_ARG, "lam required");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.alpha = GalScalar{alpha, alpha_stride};
     a.rho1 = GalScalar{lam, lam_stride};
     a.ltl = ltl; a.ltl_gstride = ltl_gstride;
     a.o0 = x;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::tikhonov(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::tikhonov(a, (hipStream_t)stream); });
 }
 
 int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, H);
+    Args a = base_args(N, ws, H, W);
     a.a0 = filt;
     a.s_hh = power_half;
-    return dispatch<Ops>(H, [&](auto op) { return decltype(op)::power(a, (hipStream_t)stream); });
+    return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::power(a, (hipStream_t)stream); });
 }
 
 namespace {
 int check_gx(int N, int H, int W) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
-    if (H != W || !gd_supported_size(2 * H, 2 * W) || H % 4)
-        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: square images of side 32, 48, 64 or 128 (2x padded grid)");
+    // pad_double (utils/utils_torch.py:11-13) doubles even sides only (an odd side gives a 2H - 1 grid
+    // whose crop_half no longer matches the image in the reference)
+    if (H != W || H % 2 || !gd_supported_size(2 * H, 2 * W) || (specialised_size(2 * H, 2 * W) && H % 4))
+        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: square images of even side 2 .. 512 (2x padded grid)");
     return GD_OK;
 }
 void bind_gx_state(Args& a, void* state, int N, int H) {
@@ -2771,12 +2793,12 @@ int gd_gx_init(const float* y, const float* psf, long long psf_gstride, int h, i
     GD_TRY(check_gx(N, H, W));
     if (h != H || w != W) return fail(GD_ERR_ARG, "UnrolledADMMGaussian pads the PSF like the image: psf must be H x W");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, 2 * H);
+    Args a = base_args(N, ws, 2 * H, 2 * W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
     a.alpha = GalScalar{alpha, alpha_stride};
     bind_gx_state(a, state, N, H);
     a.o0 = z0;
-    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_init(a, (hipStream_t)stream); });
+    return dispatch<Ops>(2 * H, 2 * W, [&](auto op) { return decltype(op)::gx_init(a, (hipStream_t)stream); });
 }
 
 int gd_gx_xupdate(const float* z, float* u, const float* x_prev, const float* rho, long long rho_stride,
@@ -2785,14 +2807,14 @@ int gd_gx_xupdate(const float* z, float* u, const float* x_prev, const float* rh
     GD_TRY(check_gx(N, H, W));
     if (x_prev && (!u || !rho_prev)) return fail(GD_ERR_ARG, "the fused dual update needs u and rho_prev");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, 2 * H);
+    Args a = base_args(N, ws, 2 * H, 2 * W);
     bind_gx_state(a, state, N, H);
     a.a0 = z; a.a1 = u; a.a2 = x_prev; a.o1 = u;
     a.rho1 = GalScalar{rho, rho_stride};
     a.rho2 = GalScalar{rho_prev ? rho_prev : rho, rho_prev ? rho_prev_stride : rho_stride};
     a.s_w = reinterpret_cast<float2*>(xspec);
     a.o0 = x; a.o2 = zin;
-    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_x(a, (hipStream_t)stream); });
+    return dispatch<Ops>(2 * H, 2 * W, [&](auto op) { return decltype(op)::gx_x(a, (hipStream_t)stream); });
 }
 
 int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho, long long rho_stride,
@@ -2801,22 +2823,22 @@ int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho
     GD_TRY(check_gx(N, H, W));
     if (!xspec) return fail(GD_ERR_ARG, "backward needs the forward's saved spectrum");
     if (N == 0) return GD_OK;
-    Args a = base_args(N, ws, 2 * H);
+    Args a = base_args(N, ws, 2 * H, 2 * W);
     bind_gx_state(a, state, N, H);
     a.a0 = grad_x; a.a1 = z;
     a.rho1 = GalScalar{rho, rho_stride};
     a.s_w = reinterpret_cast<float2*>(const_cast<void*>(xspec));
     a.o0 = grad_z; a.o1 = grad_u; a.o2 = grad_rho_part;
-    return dispatch<Ops>(2 * H, [&](auto op) { return decltype(op)::gx_x_bwd(a, (hipStream_t)stream); });
+    return dispatch<Ops>(2 * H, 2 * W, [&](auto op) { return decltype(op)::gx_x_bwd(a, (hipStream_t)stream); });
 }
 
 int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
                          void* stream) {
-    if (H != W || H <= 0 || H > 4096) return fail(GD_ERR_UNSUPPORTED, "square images only");
+    if (H <= 0 || W <= 0 || H > 4096 || W > 4096) return fail(GD_ERR_UNSUPPORTED, "image sides must be in [1, 4096]");
     if (ntaps < 0 || (ntaps > 0 && (!rc || !vals))) return fail(GD_ERR_ARG, "bad tap list");
     const int K = W / 2 + 1;
     hipLaunchKernelGGL(k_sparse_power, dim3((K * H + 255) / 256), dim3(256), 0, (hipStream_t)stream, rc, vals, ntaps,
-                       power_half, H, K);
+                       power_half, H, W, K);
     return check_launch("k_sparse_power");
 }
 

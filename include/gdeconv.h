@@ -10,7 +10,10 @@
  *     No C++ exception crosses the ABI.  Re-entrant across streams given distinct workspaces;
  *   - spectra are half spectra stored TRANSPOSED, complex64 [N][W/2+1][H] (kx-major, ky
  *     contiguous); `ws` is a workspace of gd_workspace_bytes(N, H, W) bytes;
- *   - supported sizes: square H = W in {32, 48, 64, 96, 128, 256}; PSFs square, even side <= H.
+ *   - sizes: any H x W with 2 <= H, W <= 1024 (utils/utils_torch.py's torch.fft path takes any size);
+ *     square 32/48/64/96/128/256 run compile-time-planned kernels, every other size the runtime-
+ *     planned ones (csrc/gd_generic.hpp) with the same operation chains; PSFs square, even side
+ *     <= min(H, W).
  *
  * Reference interfaces replaced (paths relative to mbertagna/Galaxy-Deconv @ 2025-03-07):
  *   gd_psf_to_otf       utils/utils_torch.py:79-92   psf_to_otf(ker, size)
@@ -53,7 +56,7 @@ extern "C" {
 int gd_abi_version(void);
 const char* gd_engine_rev(void);
 const char* gd_last_error(void);
-int gd_supported_size(int H, int W);
+int gd_supported_size(int H, int W);  /* 1 compile-time-planned, 2 runtime-planned, 0 unsupported */
 size_t gd_workspace_bytes(int N, int H, int W);
 size_t gd_otf_bytes(int N, int H, int W);
 
@@ -125,7 +128,7 @@ int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, v
 int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
                          void* stream);
 
-/* UnrolledADMMGaussian (the variant train.py trains): images H x W (H = W in {32, 48, 64, 128}) and
+/* UnrolledADMMGaussian (the variant train.py trains): images H x W (H = W, even, <= 512) and
  * PSFs of the SAME size, zero-padded to the 2H x 2W grid (pad_double) with the reference's
  * ifftshift / fftshift / crop_half expressed as origin placement (the shift is a common phase that
  * cancels).  state: gd_gx_state_bytes - |H|^2 and G = F(max(y,0)) conj(H) on the 2H grid, written

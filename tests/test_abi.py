@@ -52,7 +52,9 @@ def test_host_only_queries(lib):
     from gdeconv import _lib as _lib_mod
     assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 3
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
-    assert lib.gd_supported_size(50, 50) == 0 and lib.gd_supported_size(256, 128) == 0
+    # other sizes up to 1024 per side, square or not, run the runtime-planned kernels (2)
+    assert lib.gd_supported_size(50, 50) == 2 and lib.gd_supported_size(256, 128) == 2
+    assert lib.gd_supported_size(1, 48) == 0 and lib.gd_supported_size(48, 1025) == 0
     # workspace: N * 2 images * (W/2+1) * H complex64
     assert lib.gd_workspace_bytes(4096, 256, 256) == 4096 * 2 * 129 * 256 * 8
     assert lib.gd_otf_bytes(2, 48, 48) == 2 * 25 * 48 * 8
@@ -62,9 +64,11 @@ def test_argument_errors_need_no_device(lib):
     # validation happens before any HIP call: odd PSF, unsupported size, bad llh
     assert lib.gd_psf_to_otf(None, 0, 5, 5, 1, 48, 48, None, None, None) == -1
     assert b"even" in lib.gd_last_error()
-    assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 50, 50, None, None) == -2
+    assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 2048, 50, None, None) == -2
     assert lib.gd_admm_init(None, None, 0, 48, 48, None, 0, None, 0, 7, 1, 48, 48,
                             None, None, None, None) == -1
     # state: Gaussian |H|^2 (fp32) + conj(H)F(y/a) + F(u1) + conj(H)F(v-u2); Poisson OTF + two images
     assert lib.gd_admm_state_bytes(3, 48, 48, 0) == 3 * 25 * 48 * (4 + 3 * 8)
     assert lib.gd_admm_state_bytes(3, 48, 48, 1) == 3 * 25 * 48 * 8 + 2 * 3 * 48 * 48 * 4
+    # an odd number of |H|^2 values is padded to keep the complex arrays 8-byte aligned
+    assert lib.gd_admm_state_bytes(1, 45, 45, 0) == (23 * 45 + 1) // 2 * 8 + 3 * 23 * 45 * 8

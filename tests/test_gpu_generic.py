@@ -1,0 +1,218 @@
+"""GPU parity of the runtime-planned path (csrc/gd_generic.hpp): image sizes outside the compile-time
+set (square 32/48/64/96/128/256), square or not, odd, prime, up to 1024 per side - against the
+reference's golden vectors (tests/golden/make_golden_sizes.py) and the oracle.
+Bar: per galaxy max|out - ref| <= 1e-5 * max|ref| (fp32)."""
+import numpy as np
+import pytest
+import torch
+
+import admm_oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160)]   # sizes.npz
+FFT_SIZES = [(2, 2), (3, 5), (17, 19), (40, 40), (64, 48), (45, 60), (97, 80), (243, 125), (1000, 30),
+             (7, 1024), (1024, 1024), (96, 256), (256, 255)]
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def nerr(out, ref):
+    return float(O.normwise_error(out, ref).max())
+
+
+def report(tag, out, ref):
+    import json
+    import os
+    e = nerr(out, ref)
+    pix = float(O.pixel_error_floored(out, ref).max())
+    print(f"[parity] {tag}: normwise {e:.3e}, per-pixel (floor 1e-5 max|ref|) {pix:.3e}")
+    log = os.environ.get("GD_PARITY_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"case": tag, "normwise": e, "per_pixel_floored": pix}) + "\n")
+    return e
+
+
+@pytest.fixture(scope="module")
+def eng(dev):
+    from gdeconv import engine
+    return engine
+
+
+def load(H, W):
+    g = golden("sizes.npz")
+    t = f"{H}x{W}"
+    return g, t, T(g[f"{t}_obs"]), T(g[f"{t}_psf"]), T(g[f"{t}_alpha"])
+
+
+@pytest.mark.parametrize("H,W", FFT_SIZES)
+def test_generic_rfft2_matches_fp64(eng, dev, H, W):
+    from gdeconv import _lib
+    assert _lib.load().gd_supported_size(H, W) == (1 if H == W and H in (32, 48, 64, 96, 128, 256) else 2)
+    N = 2 if H * W <= 65536 else 1
+    x = torch.randn(N, 1, H, W, generator=torch.Generator().manual_seed(H * 7 + W))
+    spec = eng.rfft2_half(x.to(dev)).cpu()                       # [N, K, H] (kx, ky)
+    ref = torch.fft.rfft2(x.double())[:, 0].transpose(1, 2)
+    e = (spec.to(torch.complex128) - ref).abs().amax((1, 2)) / ref.abs().amax((1, 2))
+    print(f"rfft2 {H}x{W}: {float(e.max()):.2e}")
+    assert float(e.max()) < 3e-6
+    back = eng.irfft2_half(spec.to(dev), H, W).cpu()
+    assert nerr(back, x) < 3e-6
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_generic_conv_and_psf_to_otf(eng, dev, H, W):
+    g, t, obs, psf, _ = load(H, W)
+    otf = eng.psf_to_otf_half(psf.to(dev), 2, H, W)
+    _, Href = O.psf_to_otf(psf, obs.size())
+    ref_half = Href[:, 0, :, : W // 2 + 1].transpose(1, 2)
+    assert nerr(torch.view_as_real(otf.cpu()), torch.view_as_real(ref_half)) < TOL
+    assert report(f"conv_fft_batch {t}", eng.conv_half(otf, obs.to(dev)).cpu(), T(g[f"{t}_conv_H"])) < TOL
+    assert nerr(eng.conv_half(otf, obs.to(dev), conj=True).cpu(), T(g[f"{t}_conv_Ht"])) < TOL
+    # one shared OTF broadcast over the batch (fftn(x) * H with H [1,1,H,W])
+    out = eng.conv_half(otf[:1], obs.to(dev)).cpu()
+    assert nerr(out, O.conv_fft_batch(Href[:1], obs)) < TOL
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_generic_reference_layout_helpers(dev, H, W):
+    from utils.utils_torch import conv_fft_batch, psf_to_otf
+    g, t, obs, psf, _ = load(H, W)
+    kpad, Hk = psf_to_otf(psf.to(dev), obs.size())
+    kref, Href = O.psf_to_otf(psf, obs.size())
+    assert torch.equal(kpad.cpu(), kref)
+    assert nerr(torch.view_as_real(Hk.cpu()), torch.view_as_real(Href)) < TOL
+    assert nerr(conv_fft_batch(Hk, obs.to(dev)).cpu(), T(g[f"{t}_conv_H"])) < TOL
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_generic_wiener_rl_tikhonov(dev, H, W):
+    from gdeconv.models import Tikhonov
+    from models.Richard_Lucy import Richard_Lucy
+    from models.Wiener import Wiener
+    g, t, obs, psf, alpha = load(H, W)
+    o, p, a = obs.to(dev), psf.to(dev), alpha.to(dev)
+    assert report(f"Wiener {t}", Wiener()(o, p, a).cpu(), T(g[f"{t}_wiener"])) < TOL
+    assert report(f"Richard_Lucy(10) {t}", Richard_Lucy(10)(o, p).cpu(), T(g[f"{t}_rl10"])) < TOL
+    yp = torch.clamp_min(o, 0)
+    for filt in ("Identity", "Laplacian"):
+        out = Tikhonov(filter=filt)(yp, p, a, torch.tensor(0.37)).cpu()
+        assert report(f"Tikhonov({filt}) {t}", out, T(g[f"{t}_tik_{filt}"])) < TOL
+
+
+def _spectral_model(n, llh, dev, rho1, rho2):
+    from models.Unrolled_ADMM import Unrolled_ADMM
+    m = Unrolled_ADMM(n_iters=n, llh=llh).to(dev).eval()
+    m.Z = torch.nn.Identity()
+    m.rhos = lambda k, a: (rho1.to(dev), rho2.to(dev))
+    return m
+
+
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+@pytest.mark.parametrize("H,W", SIZES)
+def test_generic_admm_identity_denoiser(dev, H, W, llh):
+    g, t, obs, psf, alpha = load(H, W)
+    m = _spectral_model(4, llh, dev, T(g[f"{t}_{llh}_rho1"]), T(g[f"{t}_{llh}_rho2"]))
+    with torch.no_grad():
+        out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    assert report(f"Unrolled_ADMM(4, {llh}) identity {t}", out, T(g[f"{t}_{llh}_out"])) < TOL
+
+
+def test_generic_subnet_rhos(dev):
+    """The SubNet (engine feature kernel + MLP) on the PSFs of a generic-size batch: the rhos the
+    reference computed for the fixture."""
+    from gdeconv.weights import make_state_dict
+    from models.Unrolled_ADMM import Unrolled_ADMM
+    g, t, obs, psf, alpha = load(97, 80)
+    m = Unrolled_ADMM(n_iters=4, llh="Gaussian")
+    m.load_state_dict(make_state_dict(m, 1234))
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        r1, r2 = m.init(psf.to(dev), alpha.to(dev))
+    assert nerr(r1.cpu().reshape(2, -1), T(g[f"{t}_Gaussian_rho1"]).reshape(2, -1)) < TOL
+    assert nerr(r2.cpu().reshape(2, -1), T(g[f"{t}_Gaussian_rho2"]).reshape(2, -1)) < TOL
+
+
+def test_generic_full_model(dev):
+    """Unrolled_ADMM(n=2, 'Gaussian') with SubNet + ResUNet (seed-1234 weights) at 45 x 60."""
+    from gdeconv.weights import make_state_dict
+    from models.Unrolled_ADMM import Unrolled_ADMM
+    g = golden("sizes.npz")
+    obs, psf, alpha = (T(g[k]).to(dev) for k in ("full_obs", "full_psf", "full_alpha"))
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    m = Unrolled_ADMM(n_iters=2, llh="Gaussian")
+    m.load_state_dict(make_state_dict(m, 1234))
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        out = m(obs, psf, alpha).cpu()
+    assert report("Unrolled_ADMM(2, Gaussian) full model 45x60", out, T(g["full_out"])) < TOL
+
+
+def test_generic_gauss2x_identity(dev):
+    """UnrolledADMMGaussian(n=4) with the identity denoiser at 40 x 40 (80 x 80 padded grid)."""
+    from gdeconv.weights import make_state_dict
+    from models.unrolled_admm_gaussian import UnrolledADMMGaussian
+    g = golden("sizes.npz")
+    obs, psf, alpha, rho = (T(g[k]) for k in ("gx_obs", "gx_psf", "gx_alpha", "gx_rho"))
+    m = UnrolledADMMGaussian(n_iters=4)
+    m.load_state_dict(make_state_dict(m, 1234))
+    m.Z = torch.nn.Identity()
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        assert nerr(m.init(psf.to(dev), alpha.to(dev)).cpu().reshape(2, -1), rho.reshape(2, -1)) < TOL
+        out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    assert report("UnrolledADMMGaussian(4) identity 40x40", out, T(g["gx_out"])) < TOL
+
+
+def test_generic_gauss2x_backward(dev):
+    """The X update's HIP backward on a generic 2x grid (side 42 -> 84 x 84): forward and gradients
+    against autograd through the fp64 oracle (models/unrolled_admm_gaussian.py:89-93)."""
+    from gdeconv import engine
+    from gdeconv.synth import make_batch
+    obs, psf, alpha, _ = make_batch(2, 42, h=42, seed=9, device=dev)
+    st = engine.GaussXState(obs, psf, alpha)
+    gen = torch.Generator().manual_seed(5)
+    a, b, u = (torch.randn(obs.shape, generator=gen).to(dev) for _ in range(3))
+    rho = torch.tensor([0.7, 1.3], device=dev).view(2, 1, 1, 1)
+    z = a.clone().requires_grad_(True)
+    r = rho.clone().requires_grad_(True)
+    uu = u.clone().requires_grad_(True)
+    x = engine.gx_x_update(st, z, uu, r)
+    (x * b).sum().backward()
+    _, Y, Ht, HtH = O.gx_spectra(obs.cpu().double(), psf.cpu().double())
+    z64 = a.cpu().double().requires_grad_(True)
+    u64 = u.cpu().double().requires_grad_(True)
+    r64 = rho.cpu().double().requires_grad_(True)
+    x64 = O.gx_x_update(Y, Ht, HtH, z64, u64, r64)
+    assert nerr(x.detach().cpu(), x64.detach()) < TOL
+    (x64 * b.cpu().double()).sum().backward()
+    assert nerr(z.grad.cpu(), z64.grad) < TOL
+    assert nerr(uu.grad.cpu(), u64.grad) < TOL
+    assert float(((r.grad.cpu().double() - r64.grad).abs() / r64.grad.abs()).max()) < TOL
+
+
+def test_generic_batch_invariance_and_odd_batch(dev):
+    """Chunked pipeline over a ragged batch at a generic size: every galaxy equals its solo run."""
+    from gdeconv import _lib, engine
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 23
+    obs, psf, alpha, _ = make_batch(N, 72, 88, h=32, seed=31, device=dev)
+    old = lib.gd_set_chunk_bytes(1 << 20)  # force many chunks over the 2 pipeline streams
+    try:
+        full = engine.wiener(obs, psf, alpha).cpu()
+        rl = engine.richardson_lucy(obs, psf, 3).cpu()
+    finally:
+        lib.gd_set_chunk_bytes(old)
+    for i in (0, 11, N - 1):
+        solo = engine.wiener(obs[i:i + 1], psf[i:i + 1], alpha[i:i + 1]).cpu()
+        assert torch.equal(full[i:i + 1], solo)
+        assert torch.equal(rl[i:i + 1], engine.richardson_lucy(obs[i:i + 1], psf[i:i + 1], 3).cpu())
+    ref = O.wiener(obs[:2].cpu(), psf[:2].cpu(), alpha[:2].cpu())
+    assert nerr(full[:2], ref) < TOL

@@ -218,3 +218,43 @@ def test_gauss2x_gradients():
     assert torch.equal(out.detach(), T(g["grad_full_out"]))
     for k in ("init.mlp.4.weight", "init.mlp.4.bias", "Z.net.m_tail.weight", "Z.net.m_head.weight"):
         assert torch.equal(params[k].grad, T(g[f"grad_full_{k}"])), k
+
+
+# ------------------------------------------------------------------ sizes outside the compile-time set
+SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160)]  # tests/golden/make_golden_sizes.py
+
+
+@pytest.mark.parametrize("H,W", SIZES)
+def test_generic_sizes_spectral_ops(H, W):
+    """psf_to_otf + conv_fft_batch, Wiener, Richard_Lucy(10), Tikhonov and the identity-denoiser
+    Unrolled_ADMM(n=4) at non-square / odd / prime sizes: the oracle reproduces the reference bit for bit."""
+    torch.set_num_threads(8)
+    g = golden("sizes.npz")
+    t = f"{H}x{W}"
+    obs, psf, alpha = T(g[f"{t}_obs"]), T(g[f"{t}_psf"]), T(g[f"{t}_alpha"])
+    _, Hk = O.psf_to_otf(psf, obs.size())
+    assert torch.equal(O.conv_fft_batch(Hk, obs), T(g[f"{t}_conv_H"]))
+    assert torch.equal(O.conv_fft_batch(torch.conj(Hk), obs), T(g[f"{t}_conv_Ht"]))
+    assert torch.equal(O.wiener(obs, psf, alpha), T(g[f"{t}_wiener"]))
+    assert torch.equal(O.richardson_lucy(obs, psf, 10), T(g[f"{t}_rl10"]))
+    yp = torch.max(obs, torch.zeros_like(obs))
+    for filt in ("Identity", "Laplacian"):
+        assert torch.equal(O.tikhonov(yp, psf, alpha, torch.tensor(0.37), filt), T(g[f"{t}_tik_{filt}"]))
+    for llh in ("Gaussian", "Poisson"):
+        out = O.admm_forward(obs, psf, alpha, T(g[f"{t}_{llh}_rho1"]), T(g[f"{t}_{llh}_rho2"]), llh)
+        assert torch.equal(out, T(g[f"{t}_{llh}_out"]))
+
+
+def test_generic_size_full_model_and_gauss2x():
+    """The full Unrolled_ADMM(n=2, 'Gaussian') with the ResUNet at 45 x 60, and UnrolledADMMGaussian(n=4,
+    identity denoiser) at 40 x 40 (80 x 80 padded grid)."""
+    torch.set_num_threads(8)
+    g = golden("sizes.npz")
+    obs, psf, alpha = T(g["full_obs"]), T(g["full_psf"]), T(g["full_alpha"])
+    m = _denoiser_and_subnet(2)
+    with torch.no_grad():
+        rho1, rho2 = m.init(psf, alpha)
+        out = O.admm_forward(obs, psf, alpha, rho1, rho2, "Gaussian", denoise=m.Z)
+    assert torch.equal(out, T(g["full_out"]))
+    out = O.gx_forward(T(g["gx_obs"]), T(g["gx_psf"]), T(g["gx_alpha"]), T(g["gx_rho"]))
+    assert torch.equal(out, T(g["gx_out"]))
