@@ -6,7 +6,7 @@
 // pass -> row inverse, the chunked pipeline of for_chunks) and the same per-bin / per-pixel arithmetic,
 // on a line FFT planned at run time:
 //
-//  * Stockham autosort, mixed radix: n = 4^a 2^b 3^c p1 p2 ... (radix 2, 3, 4 as explicit butterflies,
+//  * Stockham autosort, mixed radix: n = 4^a 2^b 3^c 5^d p1 p2 ... (radix 2, 3, 4, 5 as explicit butterflies,
 //    any other prime factor as a direct DFT of that length), all lines of a workgroup transformed in
 //    LDS, ping-pong between two line buffers, one barrier per stage;
 //  * twiddles W_n^k = exp(-2 pi i k / n) for k < n computed per workgroup in double (sincospi) and
@@ -119,16 +119,38 @@ __device__ float2* fft_lines(float2* x, float2* y, const Axis& ax, const float2*
                 ys[0] = cadd(a0, sm);
                 ys[p] = cadd(t, u);
                 ys[2 * p] = csub(t, u);
+            } else if (r == 5) {
+                const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv)),
+                             a3 = cmul(xs[3 * m], twv(tw, 3 * e1, inv)), a4 = cmul(xs[4 * m], twv(tw, 4 * e1, inv));
+                const float c1 = 0.309016994374947424102f, c2 = -0.809016994374947424102f;  // cos(2pi/5), cos(4pi/5)
+                const float s1 = 0.951056516295153572116f, s2 = 0.587785252292473129169f;   // sin(2pi/5), sin(4pi/5)
+                const float2 b1 = cadd(a1, a4), b2 = cadd(a2, a3), d1 = csub(a1, a4), d2 = csub(a2, a3);
+                const float2 t1 = make_float2(a0.x + c1 * b1.x + c2 * b2.x, a0.y + c1 * b1.y + c2 * b2.y);
+                const float2 t2 = make_float2(a0.x + c2 * b1.x + c1 * b2.x, a0.y + c2 * b1.y + c1 * b2.y);
+                const float2 u1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
+                const float2 u2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
+                // forward: X1 = t1 - i u1, X4 = t1 + i u1, X2 = t2 - i u2, X3 = t2 + i u2 (inverse: i -> -i)
+                const float2 iu1 = inv ? make_float2(-u1.y, u1.x) : make_float2(u1.y, -u1.x);
+                const float2 iu2 = inv ? make_float2(-u2.y, u2.x) : make_float2(u2.y, -u2.x);
+                ys[0] = cadd(a0, cadd(b1, b2));
+                ys[p] = cadd(t1, iu1);
+                ys[2 * p] = cadd(t2, iu2);
+                ys[3 * p] = csub(t2, iu2);
+                ys[4 * p] = csub(t1, iu1);
             } else {
-                // direct DFT of prime length r: X_q = sum_t x_t W_n^{t (e1 + q m)}
+                // direct DFT of prime length r: X_q = sum_t x_t W_n^{t (e1 + q m)}, the twiddle index
+                // advanced by step (< n) and reduced by one compare per term
                 for (int q = 0; q < r; ++q) {
                     float2 acc = make_float2(0.f, 0.f);
                     const int step = e1 + q * m;
+                    int e = 0;
                     for (int t = 0; t < r; ++t) {
-                        const float2 w = twv(tw, (t * step) % n, inv);
+                        const float2 w = twv(tw, e, inv);
                         const float2 v = xs[t * m];
                         acc.x = fmaf(v.x, w.x, fmaf(-v.y, w.y, acc.x));
                         acc.y = fmaf(v.x, w.y, fmaf(v.y, w.x, acc.y));
+                        e += step;
+                        if (e >= n) e -= n;
                     }
                     ys[q * p] = acc;
                 }
