@@ -292,7 +292,8 @@ def main():
     lib.gd_set_fused_init(fused_init)
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
-    use_fused = bool(fused) and args.size in (32, 48, 64, 96, 128, 256) and args.llh == "Gaussian"
+    generic = args.size not in (32, 48, 64, 96, 128, 256)  # gd_supported_size == 2: gd_generic.hpp
+    use_fused = bool(fused) and not generic and args.llh == "Gaussian"
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
@@ -504,12 +505,15 @@ def main():
     if rl:
         metric = f"galaxies/sec ({L}x{L}, Richard_Lucy n_iters={n})"
         workload = (f"Richard_Lucy(n_iters={n}) forward (OTF + {n} multiplicative FFT-conv iterations), "
-                    f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[4])")
+                    f"batch {N}/GPU, {L}x{L} fp32" + (" (BASELINE.json configs[4])" if L == 256 and n == 100 else ""))
     else:
         metric = f"galaxies/sec ({L}x{L}, n_iters={n}) - unrolled ADMM spectral engine"
         workload = (f"Unrolled_ADMM(n_iters={n}, llh='{args.llh}') forward, denoiser=identity "
                     f"(spectral engine: SubNet + OTF + init_l2 + {n} ADMM iterations), "
-                    f"batch {N}/GPU, {L}x{L} fp32 (BASELINE.json configs[2]/[3])")
+                    f"batch {N}/GPU, {L}x{L} fp32" + (" (BASELINE.json configs[2]/[3])" if L == 256 else
+                                                      " (BASELINE.json configs[1])" if L == 48 else
+                                                      " (not a BASELINE config: runtime-planned size)" if generic
+                                                      else " (not a BASELINE config)"))
 
     rec = {
         "metric": metric,
@@ -528,14 +532,15 @@ def main():
                                  if use_fused else (rl_impl if rl else
                                                     ("two whole-galaxy passes: k_gal_reg<POIS> (X update, u1, zin) + "
                                                      "k_pois_b (Hx, V step, duals, conj(H) F(w))") if pois2
-                                                    else "three-kernel")),
+                                                    else "three-kernel, runtime-planned line FFTs (gd_generic.hpp)"
+                                                    if generic else "three-kernel")),
                    "init": (None if rl else
                             ("fused, " + INIT_IMPL[fused_init] if fused_init else "chunked")
                             if (L == 256 and args.llh == "Gaussian") else
                             (("k_psf_rows + k_gal_reg_init<POIS>" if fused_init else "chunked Gaussian chain")
                              + " + k_pois_b<INIT>") if pois2 else
                             ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
-                             else "chunked"))},
+                             and not generic else "chunked" + (", runtime-planned line FFTs" if generic else "")))},
         "roofline": roofline,
         # SURVEY.md 8(d)'s per-galaxy byte model prices the reference's op-for-op path (16 fp32 words per
         # pixel per iteration); this engine's compulsory traffic is 7.5 (roofline above), so the survey
