@@ -59,6 +59,7 @@ MODE_NAMES = {
     "k_row_inv": ["ITER", "INIT", "OUT1", "OUT2", "RL_FINAL"],
     "k_row_invfwd": ["CLAMP", "RL_RATIO", "RL_UPDATE"],
     "k_subnet_features": ["FEATURES", "PSF"],
+    "k_subnet_rhos": ["-", "-", "FUSED"],
     "k_subnet_mlp": ["MLP"],
     "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],

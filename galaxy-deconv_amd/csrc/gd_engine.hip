@@ -2211,6 +2211,10 @@ int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations at 256^2: 1 = k_gal_reg, 2 = k_gal_iter2, 3 = k_gal_iter (parking); 0 = chunked
 int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per galaxy), 0 = chunked chain
+// gd_subnet_rhos_psf: one fused launch per galaxy up to this batch (one round of workgroups on the 256 CUs:
+// 60.5 vs 75.5 us at 256 x 48^2), else the feature kernel + batched MLP (1024: 173 vs 212 us; 4096: 584 vs
+// 818 us fused - each fused workgroup re-reads the MLP weights, and 129 VGPRs allow one per CU)
+int g_subnet_fused_max = 256;
 int g_fused_init = 1;  // Gaussian init at 256^2 (+ k_psf_rows<STATE>): 1 = k_gal_reg_init, 2 = k_gal_iter<KM = 1> +
                        // k_gal_w1, 3 = k_gal_iter<KM = 3>; 0 = chunked
 
@@ -2908,6 +2912,12 @@ int gd_set_fused_rl(int on) {
     return old;
 }
 
+int gd_set_subnet_fused_max(int n) {
+    const int old = g_subnet_fused_max;
+    if (n >= 0) g_subnet_fused_max = n;
+    return old;
+}
+
 int gd_set_fused_iteration(int on) {
     const int old = g_fused;
     g_fused = (on >= 1 && on <= 3) ? on : 0;
@@ -2940,6 +2950,12 @@ int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const flo
     if (n_out < 1 || n_out > gd::subnet::kMaxOut) return fail(GD_ERR_ARG, "n_out must be in [1, 64]");
     if (h < 2 || h > gd::subnet::kPsfMaxH || (h & 1)) return fail(GD_ERR_UNSUPPORTED, "PSF side must be even and <= 64");
     if (N == 0) return GD_OK;
+    if (N <= g_subnet_fused_max) {  // features + MLP per galaxy in one workgroup (bit-identical rhos)
+        ProfScope ps("k_subnet_rhos<128,2>", (hipStream_t)stream, 1);
+        hipLaunchKernelGGL(gd::subnet::k_subnet_rhos_psf, dim3(N), dim3(gd::subnet::kThreads), 0, (hipStream_t)stream,
+                           psf, psf_gstride, h, params, mlp_params, alpha, alpha_stride, rhos, n_out, N);
+        return check_launch("k_subnet_rhos_psf");
+    }
     {
         ProfScope ps("k_subnet_features<128,1>", (hipStream_t)stream, 1);
         hipLaunchKernelGGL(gd::subnet::k_subnet_features_psf, dim3(N), dim3(gd::subnet::kThreads), 0,

@@ -201,6 +201,13 @@ int gd_set_fused_iteration(int on);
  * process-wide. */
 int gd_set_fused_rl(int on);
 
+/* SubNet from the PSFs (gd_subnet_rhos_psf): batches of at most n galaxies run features + MLP in ONE
+ * launch, one workgroup per galaxy (each reads the MLP weights from L2; `feat` is not written); larger
+ * batches run the feature kernel and the batched MLP kernel (8 galaxies per workgroup).  The rhos are
+ * bit-identical either way (same summation order).  Default 256; n < 0 only queries.  Returns the
+ * previous value. */
+int gd_set_subnet_fused_max(int n);
+
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->

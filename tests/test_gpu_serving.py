@@ -137,3 +137,30 @@ def test_device_batches_feed_the_engine(dev, packed_golden):
         direct = m(torch.from_numpy(g["obs_raw"][:, None]).to(dev), torch.from_numpy(g["psf_raw"][:, None]).to(dev),
                    torch.from_numpy(np.concatenate([g["train_alpha"], g["test_alpha"]])).to(dev))
     assert torch.equal(torch.cat(outs), direct)
+
+
+@pytest.mark.parametrize("N", [1, 37, 256, 1100])
+def test_subnet_fused_launch_bit_identical(dev, N):
+    """gd_subnet_rhos_psf: the one-launch per-galaxy SubNet (features + MLP in one workgroup, batches up
+    to gd_set_subnet_fused_max) gives the same bits as the feature kernel + batched MLP kernel."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    from gdeconv.weights import make_state_dict
+    from models.Unrolled_ADMM import Unrolled_ADMM
+    lib = _lib.load()
+    m = Unrolled_ADMM(n_iters=8, llh="Gaussian")
+    m.load_state_dict(make_state_dict(m, 1234))
+    m = m.to(dev).eval()
+    _, psf, alpha, _ = make_batch(N, 48, seed=900 + N, device=dev)
+    old = lib.gd_set_subnet_fused_max(-1)
+    outs = []
+    try:
+        for thr in (1 << 30, 0):
+            lib.gd_set_subnet_fused_max(thr)
+            with torch.no_grad():
+                r1, r2 = m.init(psf, alpha)
+            outs.append(torch.cat([r1.flatten(), r2.flatten()]).cpu())
+    finally:
+        lib.gd_set_subnet_fused_max(old)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
