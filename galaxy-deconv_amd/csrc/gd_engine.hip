@@ -1645,6 +1645,15 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
     float2* my = xch + line * XCH;
     fill_twiddles<L>(tw, tid, 256);
     const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    // the state of this line's first column, loaded now so that its latency hides behind phase R (at
+    // 48^2 one workgroup per CU: the launch is a latency chain, not a bandwidth one)
+    constexpr bool PRE = L <= 64;  // 96^2 / 128^2 (24 / 16 points per lane): registers are short
+    GState pre[PRE ? F2 : 1];
+    if (PRE && line < K) {
+        const size_t ob = ((size_t)g * K + line) * L + j;
+#pragma unroll
+        for (int s = 0; s < (PRE ? F2 : 0); ++s) pre[s] = gauss_load<L, FIRST, LAST>(a, ob + F1 * s);
+    }
     __syncthreads();
 
     // R: row pair p -> FFT -> the two rows' half spectra into S (transposed)
@@ -1665,8 +1674,15 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
         for (int s = 0; s < F2; ++s) v[s] = S[kx * L + j + F1 * s];
         line_fft<L, false>(v, j, my, tw);
         const size_t ob = ((size_t)g * K + kx) * L + j;
+        if (PRE && kx == line) {
 #pragma unroll
-        for (int s = 0; s < F2; ++s) v[s] = gauss_iter_elem<L, FIRST, LAST>(a, ob + F1 * s, v[s], r1, r2, r2n, true, inv_n);
+            for (int s = 0; s < (PRE ? F2 : 0); ++s)
+                v[s] = gauss_iter_st<L, FIRST, LAST>(a, ob + F1 * s, v[s], pre[s], r1, r2, r2n, true, inv_n);
+        } else {
+#pragma unroll
+            for (int s = 0; s < F2; ++s)
+                v[s] = gauss_iter_elem<L, FIRST, LAST>(a, ob + F1 * s, v[s], r1, r2, r2n, true, inv_n);
+        }
         line_fft<L, true>(v, j, my, tw);
 #pragma unroll
         for (int s = 0; s < F2; ++s) S[kx * L + j + F1 * s] = v[s];
