@@ -28,6 +28,14 @@ constexpr int kParams = woff(8);  // 9,172 floats
 #define GD_SN_THREADS 512  // measured: 256 -> 512 threads per galaxy: 119 -> 74 us at 256 x 48^2, 927 -> 659 us at 4096
 #endif
 constexpr int kThreads = GD_SN_THREADS;
+// Optional per-workgroup phase timestamps (tools/kbench_subnet.hip builds with GD_SN_TRACE=1).
+#if GD_SN_TRACE
+__device__ unsigned long long* g_sn_trace;
+#define SN_TRACE(k) \
+    if (tid == 0) g_sn_trace[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define SN_TRACE(k)
+#endif
 constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
 constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 
@@ -150,7 +158,8 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     const float* P = params;
 #define GD_SN_LAYER(l, CI, CO, S, POOL, IN, OUT)                                                   \
     conv_layer<CI, CO, S, POOL>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);           \
-    __syncthreads();
+    __syncthreads();                                                                             \
+    SN_TRACE(3 + l);
     GD_SN_LAYER(0, 1, 4, 64, false, A, B)      // B[4][64][64]
     GD_SN_LAYER(1, 4, 4, 64, true, B, A)       // A[4][32][32]   (+ MaxPool of Down(4,8))
     GD_SN_LAYER(2, 4, 8, 32, false, A, B)      // B[8][32][32]
@@ -161,6 +170,7 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
 #undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
     conv_layer<16, 16, 8, false>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+    SN_TRACE(10);
 }
 
 __global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __restrict__ otf128,
@@ -189,6 +199,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
     float2* tw = S2 + 10112;
     float2* Z = S2 + 4352;
     float* M = AB + 4096;
+    SN_TRACE(0);
     fill_twiddles<L>(tw, tid, kThreads);
     const int line = tid / F1, j = tid - line * F1;
     __syncthreads();
@@ -250,6 +261,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
         for (int r = 0; r < F2; ++r) m[r] = c[r].x * c[r].x + c[r].y * c[r].y;
     }
     __syncthreads();  // exchange areas -> M
+    SN_TRACE(1);
 #pragma unroll
     for (int r = 0; r < F2; ++r) {
         const int ky = j + F1 * r;
@@ -273,6 +285,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
         AB[ii * 64 + jj] = mx;
     }
     __syncthreads();
+    SN_TRACE(2);
 }
 
 __global__ __launch_bounds__(kThreads) void k_subnet_features_psf(const float* __restrict__ psf, long long psf_gstride,
@@ -437,6 +450,7 @@ __global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __res
             rhos[(size_t)g * n_out + o] = (v3 > 20.f ? v3 : log1pf(expf(v3))) + 1e-6f;
         }
     }
+    SN_TRACE(11);
 }
 
 }  // namespace subnet
