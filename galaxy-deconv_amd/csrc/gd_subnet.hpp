@@ -7,8 +7,9 @@
 // only changes phases, so |OTF|^2 equals |FFT2(F.pad(psf))|^2 of :79-83; the full 128 x 128 map is
 // read through Hermitian symmetry |H(ky,kx)|^2 = |H(-ky,-kx)|^2.  BatchNorm (eval) is folded into
 // the conv weights on the host.  Activations live in LDS (80 KiB: two workgroups per CU); a thread
-// owns an output pixel and a block of its output channels in registers, so each input value is
-// read once per channel block and the weights are wave-uniform (scalar loads).
+// owns a 2 x 2 block of output pixels (one pixel in the 8 x 8 layers) and a block of its output
+// channels in registers, so each input value is read once per channel block and the weights are
+// wave-uniform (scalar loads, tap-major so channel pairs are SGPR pairs).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -36,6 +37,9 @@ __device__ unsigned long long* g_sn_trace;
 #else
 #define SN_TRACE(k)
 #endif
+#ifndef GD_SN_QUAD
+#define GD_SN_QUAD 1  // the non-pooled layers 0, 2, 4 in 2 x 2 blocks (0: one pixel per work item)
+#endif
 constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
 constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 
@@ -48,8 +52,13 @@ constexpr int csplit(int npix, int cout) {
     return c;
 }
 
-// acc[k] = b[c0+k] + sum_ci,dy,dx w[c0+k][ci][dy][dx] in[ci][y+dy-1][x+dx-1]   (zero padding)
-template <int CIN, int CPT, int S>
+// Weights are tap-major, [cin][3][3][cout] (then bias [cout]): the CPT output channels of one tap are
+// contiguous, so one scalar load brings them and channel pairs feed packed FMAs straight from SGPR pairs
+// (with the [cout][cin][3][3] layout the pairs were 9 floats apart: SGPR spills to VGPR lanes and moves).
+__device__ __forceinline__ constexpr int wtap(int ci, int dy, int dx, int cout) { return ((ci * 3 + dy) * 3 + dx) * cout; }
+
+// acc[k] = b[c0+k] + sum_ci,dy,dx w[ci][dy][dx][c0+k] in[ci][y+dy-1][x+dx-1]   (zero padding)
+template <int CIN, int COUT, int CPT, int S>
 __device__ __forceinline__ void conv_pixel(const float* in, const float* __restrict__ w,
                                            const float* __restrict__ b, int c0, int y, int x, float (&acc)[CPT]) {
 #pragma unroll
@@ -64,28 +73,30 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
                 const int xx = x + dx - 1;
                 const float v = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
 #pragma unroll
-                for (int k = 0; k < CPT; ++k) acc[k] = fmaf(w[(((c0 + k) * CIN + ci) * 3 + dy) * 3 + dx], v, acc[k]);
+                for (int k = 0; k < CPT; ++k) acc[k] = fmaf(w[wtap(ci, dy, dx, COUT) + c0 + k], v, acc[k]);
             }
         }
     }
 }
 
 // conv3x3 + bias + ReLU (+ MaxPool2d(2) when POOL, i.e. the pool that opens the next Down block):
-// in [CIN][S][S] -> out [COUT][S'][S'] (S' = S or S/2), LDS or global.
-template <int CIN, int COUT, int S, bool POOL>
+// in [CIN][S][S] -> out [COUT][S'][S'] (S' = S or S/2), LDS or global.  QUAD (always when POOL): a work
+// item computes the 2 x 2 conv outputs of one block from one 4 x 4 input window, 16 LDS reads per input
+// channel instead of 4 x 9 and 4 CPT independent accumulators.  Every output's fma order (bias, then
+// ci, dy, dx) is conv_pixel's in both forms, so the features do not depend on the form.
+template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL>
 __device__ __forceinline__ void conv_layer(const float* in, float* out, const float* __restrict__ w,
                                            const float* __restrict__ b, int tid) {
+    static_assert(QUAD || !POOL, "the pooled layers compute 2 x 2 blocks");
     constexpr int SO = POOL ? S / 2 : S;
-    constexpr int NPIX = SO * SO;
-    constexpr int CS = csplit(NPIX, COUT), CPT = COUT / CS;
-    for (int it = tid; it < NPIX * CS; it += kThreads) {
-        const int grp = it / NPIX, p = it - grp * NPIX;
+    constexpr int SI = QUAD ? S / 2 : S;  // work items per row
+    constexpr int NITEM = SI * SI;
+    constexpr int CS = csplit(NITEM, COUT), CPT = COUT / CS;
+    for (int it = tid; it < NITEM * CS; it += kThreads) {
+        const int grp = it / NITEM, p = it - grp * NITEM;
         const int c0 = __builtin_amdgcn_readfirstlane(grp * CPT);
-        const int oy = p / SO, ox = p - oy * SO;
-        float res[CPT];
-        if constexpr (POOL) {
-            // the 2 x 2 conv outputs under one pool window share a 4 x 4 input window: 16 LDS reads
-            // per input channel instead of 4 x 9 (same fma order per output as conv_pixel)
+        const int oy = p / SI, ox = p - oy * SI;
+        if constexpr (QUAD) {
             float acc[4][CPT];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -103,27 +114,36 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
                         win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
                     }
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                    for (int dy = 0; dy < 3; ++dy)
+                    for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-                        for (int dx = 0; dx < 3; ++dx)
+                        for (int q = 0; q < 4; ++q)
 #pragma unroll
                             for (int k = 0; k < CPT; ++k)
-                                acc[q][k] = fmaf(w[(((c0 + k) * CIN + ci) * 3 + dy) * 3 + dx],
-                                                 win[(q >> 1) + dy][(q & 1) + dx], acc[q][k]);
+                                acc[q][k] = fmaf(w[wtap(ci, dy, dx, COUT) + c0 + k], win[(q >> 1) + dy][(q & 1) + dx],
+                                                 acc[q][k]);
             }
+            if constexpr (POOL) {
 #pragma unroll
-            for (int k = 0; k < CPT; ++k)   // ReLU outputs are >= 0
-                res[k] = fmaxf(fmaxf(fmaxf(0.f, acc[0][k]), fmaxf(0.f, acc[1][k])),
-                               fmaxf(fmaxf(0.f, acc[2][k]), fmaxf(0.f, acc[3][k])));
+                for (int k = 0; k < CPT; ++k)  // ReLU outputs are >= 0
+                    out[((c0 + k) * SO + oy) * SO + ox] =
+                        fmaxf(fmaxf(fmaxf(0.f, acc[0][k]), fmaxf(0.f, acc[1][k])),
+                              fmaxf(fmaxf(0.f, acc[2][k]), fmaxf(0.f, acc[3][k])));
+            } else {
+#pragma unroll
+                for (int k = 0; k < CPT; ++k)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        *reinterpret_cast<float2*>(out + ((c0 + k) * S + 2 * oy + h) * S + 2 * ox) =
+                            make_float2(fmaxf(acc[2 * h][k], 0.f), fmaxf(acc[2 * h + 1][k], 0.f));
+            }
         } else {
-            conv_pixel<CIN, CPT, S>(in, w, b, c0, oy, ox, res);
+            float res[CPT];
+            conv_pixel<CIN, COUT, CPT, S>(in, w, b, c0, oy, ox, res);
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) res[k] = fmaxf(res[k], 0.f);
+            for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * SO + ox] = fmaxf(res[k], 0.f);
         }
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * SO + ox] = res[k];
     }
 }
 
@@ -156,17 +176,17 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
 // the four Down blocks from the pooled |H|^2 in A[64][64]
 __device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
     const float* P = params;
-#define GD_SN_LAYER(l, CI, CO, S, POOL, IN, OUT)                                                   \
-    conv_layer<CI, CO, S, POOL>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);           \
+#define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT)                                             \
+    conv_layer<CI, CO, S, POOL, QUAD>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);     \
     __syncthreads();                                                                             \
     SN_TRACE(3 + l);
-    GD_SN_LAYER(0, 1, 4, 64, false, A, B)      // B[4][64][64]
-    GD_SN_LAYER(1, 4, 4, 64, true, B, A)       // A[4][32][32]   (+ MaxPool of Down(4,8))
-    GD_SN_LAYER(2, 4, 8, 32, false, A, B)      // B[8][32][32]
-    GD_SN_LAYER(3, 8, 8, 32, true, B, A)       // A[8][16][16]   (+ MaxPool of Down(8,16))
-    GD_SN_LAYER(4, 8, 16, 16, false, A, B)     // B[16][16][16]
-    GD_SN_LAYER(5, 16, 16, 16, true, B, A)     // A[16][8][8]    (+ MaxPool of Down(16,16))
-    GD_SN_LAYER(6, 16, 16, 8, false, A, B)     // B[16][8][8]
+    GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B)   // B[4][64][64]
+    GD_SN_LAYER(1, 4, 4, 64, true, true, B, A)          // A[4][32][32]   (+ MaxPool of Down(4,8))
+    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B)   // B[8][32][32]
+    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A)          // A[8][16][16]   (+ MaxPool of Down(8,16))
+    GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B)  // B[16][16][16]
+    GD_SN_LAYER(5, 16, 16, 16, true, true, B, A)        // A[16][8][8]    (+ MaxPool of Down(16,16))
+    GD_SN_LAYER(6, 16, 16, 8, false, false, A, B)       // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
 #undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
     conv_layer<16, 16, 8, false>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);

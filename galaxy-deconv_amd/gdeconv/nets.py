@@ -199,7 +199,8 @@ class SubNet(nn.Module):
                                  nn.Linear(64, self.n_out), nn.Softplus())
 
     def _packed_params(self):
-        """Folded conv+BN weights of the 8 convs in gd_subnet_features order: per layer w then b."""
+        """Folded conv+BN weights of the 8 convs in gd_subnet_features order: per layer w then b, w
+        tap-major ``[cin][3][3][cout]`` (include/gdeconv.h)."""
         key = tuple(dc._fold_key() for dc in self._double_convs())
         if getattr(self, "_pack", None) is None or self._pack[0] != key:
             with torch.no_grad():
@@ -208,7 +209,7 @@ class SubNet(nn.Module):
                     c1, b1, _, c2, b2, _ = dc.double_conv
                     for conv, bn in ((c1, b1), (c2, b2)):
                         w, b = _fold_conv_bn(conv, bn)
-                        parts += [w.reshape(-1), b.reshape(-1)]
+                        parts += [w.permute(1, 2, 3, 0).reshape(-1), b.reshape(-1)]
                 self._pack = (key, torch.cat(parts).float().contiguous())
         return self._pack[1]
 

@@ -156,8 +156,8 @@ int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho
  * of the PSFs (gd_psf_to_otf with H = W = 128; |OTF|^2 = |FFT2(pad128(psf))|^2), MaxPool2 and the
  * four Down blocks' 8 conv3x3 + ReLU layers (BatchNorm folded in) -> feat [N][1024] in the
  * reference's flatten order.  params: gd_subnet_param_count() floats, per conv layer l = 0..7
- * (cin,cout) = (1,4),(4,4),(4,8),(8,8),(8,16),(16,16),(16,16),(16,16): weights [cout][cin][3][3]
- * then bias [cout]. */
+ * (cin,cout) = (1,4),(4,4),(4,8),(8,8),(8,16),(16,16),(16,16),(16,16): weights tap-major
+ * [cin][3][3][cout] (nn.Conv2d's [cout][cin][3][3] permuted (1, 2, 3, 0)) then bias [cout]. */
 int gd_subnet_param_count(void);
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream);
 
