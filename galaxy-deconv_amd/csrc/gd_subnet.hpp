@@ -40,6 +40,12 @@ __device__ unsigned long long* g_sn_trace;
 #ifndef GD_SN_QUAD
 #define GD_SN_QUAD 1  // the non-pooled layers 0, 2, 4 in 2 x 2 blocks (0: one pixel per work item)
 #endif
+#ifndef GD_SN_UNROLL_PX
+#define GD_SN_UNROLL_PX 2  // input channels per unrolled step: per-pixel layers
+#endif
+#ifndef GD_SN_UNROLL_Q
+#define GD_SN_UNROLL_Q 2   // 2 x 2-block layers
+#endif
 constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
 constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 
@@ -63,7 +69,7 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
                                            const float* __restrict__ b, int c0, int y, int x, float (&acc)[CPT]) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) acc[k] = b[c0 + k];
-#pragma unroll 2
+#pragma unroll GD_SN_UNROLL_PX
     for (int ci = 0; ci < CIN; ++ci) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy) {
@@ -103,7 +109,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 #pragma unroll
                 for (int k = 0; k < CPT; ++k) acc[q][k] = b[c0 + k];
             const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
-#pragma unroll 2
+#pragma unroll GD_SN_UNROLL_Q
             for (int ci = 0; ci < CIN; ++ci) {
                 float win[4][4];
 #pragma unroll
@@ -209,10 +215,16 @@ __global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __re
 // 128 x 128 grid instead of F.pad's centred placement (:79-81).  Rows: 32 lines of 8 lanes transform
 // the packed row pairs (rows 2l + i 2l+1, zero beyond h); columns: 64 lines, line kx (< 64) one half-
 // spectrum column (its rows split out of the packed pairs), line 0 columns 0 and 64 (both real) packed;
-// |H|^2 of the 65 columns -> M [128][65], then MaxPool2 of the full map via Hermitian symmetry -> A.
+// |H|^2 of the 65 columns -> M [128][kMS], then MaxPool2 of the full map via Hermitian symmetry -> A.
 // LDS (float2 units of the 80 KiB A | B union): exchange areas [0, 64 x 136), packed row spectra
-// [4352, 8448), M (floats) [4096, 12416), twiddles [10112, 10240); the conv stack overwrites them all.
+// [4352, 8448), M (floats, rows of kMS) [4096, 4096 + 128 kMS), twiddles [10112, 10240); the conv stack
+// overwrites them all.  Bank-conflict-free LDS traffic around M (64 banks): row stride kMS = 72 puts a
+// wave's column-FFT results (lanes j + 8 line at rows j + 8 r, column line) in 64 distinct banks (the
+// stride 65 shared 15), and the pool's lanes take consecutive output columns so its stores are
+// contiguous (lanes on consecutive rows all hit one bank: 64-way).
 constexpr int kPsfMaxH = 64;
+constexpr int kMS = 72;
+static_assert(4096 + 128 * kMS <= 2 * 10112, "M below the twiddles");
 __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, float* AB, int tid) {
     constexpr int L = 128, F1 = 8, F2 = 16, XCH = F1 * (F2 + 1);
     float2* S2 = reinterpret_cast<float2*>(AB);
@@ -285,13 +297,13 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
 #pragma unroll
     for (int r = 0; r < F2; ++r) {
         const int ky = j + F1 * r;
-        M[ky * 65 + kx] = m[r];
-        if (line == 0) M[ky * 65 + 64] = m64[r];
+        M[ky * kMS + kx] = m[r];
+        if (line == 0) M[ky * kMS + 64] = m64[r];
     }
     __syncthreads();
     // MaxPool2d(2) of the full 128 x 128 |H|^2 -> A[64][64] (as k_subnet_features' first stage)
     for (int p = tid; p < 64 * 64; p += kThreads) {
-        const int jj = p >> 6, ii = p & 63;
+        const int ii = p >> 6, jj = p & 63;
         float mx = 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -300,7 +312,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
                 kxx = 128 - kxx;
                 ky = (128 - ky) & 127;
             }
-            mx = e == 0 ? M[ky * 65 + kxx] : fmaxf(mx, M[ky * 65 + kxx]);
+            mx = e == 0 ? M[ky * kMS + kxx] : fmaxf(mx, M[ky * kMS + kxx]);
         }
         AB[ii * 64 + jj] = mx;
     }
