@@ -1,0 +1,6 @@
+# SubNet pool-stage layout (tag = $1): kbench + trace, SubNet GPU tests, 48^2 bench.
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; T=${1:-r02}; mkdir -p $O
+timeout -k 10 60 $R/tools/kbench_subnet 4096 256 20 > $O/ksn_$T.txt 2>&1 &&
+timeout -k 10 60 $R/tools/kbench_subnet_trace 4096 256 5 >> $O/ksn_$T.txt 2>&1 &&
+cd $R && timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q -rA --timeout 120 --timeout-method thread -k "subnet or full or admm48 or configs" > $O/sn_tests_$T.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --size 48 --batch 256 --no-e2e --no-ingest --no-cpu-baseline > $O/bench48_$T.json 2> $O/bench48_$T.err
