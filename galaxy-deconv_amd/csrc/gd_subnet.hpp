@@ -240,7 +240,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
 #pragma unroll
         for (int r = 0; r < F2; ++r) {
             const int c = j + F1 * r;
-            const bool in = 2 * line < h && c < h;
+            const bool in = r < kPsfMaxH / F1 && 2 * line < h && c < h;  // r >= 8: compile-time zeros (h <= 64)
             v[r] = in ? make_float2(psf[(2 * line) * h + c], psf[(2 * line + 1) * h + c]) : make_float2(0.f, 0.f);
         }
         line_fft<L, false>(v, j, S2 + line * XCH, tw);
@@ -258,7 +258,7 @@ __device__ __forceinline__ void psf_pool(const float* __restrict__ psf, int h, f
     for (int r = 0; r < F2; ++r) {
         const int i = j + F1 * r;
         float2 val = make_float2(0.f, 0.f);
-        if (i < h) {
+        if (r < kPsfMaxH / F1 && i < h) {  // r >= 8: compile-time zeros (h <= 64)
             const float2* zp = Z + (i >> 1) * L;
             if (line == 0) {
                 const float2 z0 = zp[0], z64 = zp[L / 2];
