@@ -40,6 +40,15 @@ __device__ unsigned long long* g_sn_trace;
 #ifndef GD_SN_QUAD
 #define GD_SN_QUAD 1  // the non-pooled layers 0, 2, 4 in 2 x 2 blocks (0: one pixel per work item)
 #endif
+// Output-channel split of the 16-channel layers at 16^2 / 8^2 (layers 5, 6, 7: 64 work items per channel
+// group).  Batched launches (two workgroups per CU, many rounds) cap it at 4 groups of 4 channels: half
+// the waves idle in those layers, but each window read feeds twice the FMAs and the other workgroup
+// fills the CU (features at 4096: 417 -> 393 us).  One round of workgroups (k_subnet_rhos_psf, <= 256
+// galaxies, latency-bound) keeps 8 groups of 2 (42.8 -> 41.7 us at 256).  profiles/r02z_ksubnet_cs.txt
+#ifndef GD_SN_CS_BATCHED
+#define GD_SN_CS_BATCHED 4
+#endif
+constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #ifndef GD_SN_UNROLL_PX
 #define GD_SN_UNROLL_PX 2  // input channels per unrolled step: per-pixel layers
 #endif
@@ -52,9 +61,9 @@ constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 // Output channels are split over CS thread groups when a layer has fewer than 256 output pixels;
 // a group is 64 consecutive work items, i.e. one wave, so its channel offset is wave-uniform and the
 // weights come through scalar loads.
-constexpr int csplit(int npix, int cout) {
+constexpr int csplit(int npix, int cout, int cmax = 64) {
     int c = 1;
-    while (npix * c < kThreads && c < cout) c *= 2;
+    while (npix * c < kThreads && c < cout && c < cmax) c *= 2;
     return c;
 }
 
@@ -90,14 +99,14 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
 // item computes the 2 x 2 conv outputs of one block from one 4 x 4 input window, 16 LDS reads per input
 // channel instead of 4 x 9 and 4 CPT independent accumulators.  Every output's fma order (bias, then
 // ci, dy, dx) is conv_pixel's in both forms, so the features do not depend on the form.
-template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL>
+template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL, int CMAX = 64>
 __device__ __forceinline__ void conv_layer(const float* in, float* out, const float* __restrict__ w,
                                            const float* __restrict__ b, int tid) {
     static_assert(QUAD || !POOL, "the pooled layers compute 2 x 2 blocks");
     constexpr int SO = POOL ? S / 2 : S;
     constexpr int SI = QUAD ? S / 2 : S;  // work items per row
     constexpr int NITEM = SI * SI;
-    constexpr int CS = csplit(NITEM, COUT), CPT = COUT / CS;
+    constexpr int CS = csplit(NITEM, COUT, CMAX), CPT = COUT / CS;
     for (int it = tid; it < NITEM * CS; it += kThreads) {
         const int grp = it / NITEM, p = it - grp * NITEM;
         const int c0 = __builtin_amdgcn_readfirstlane(grp * CPT);
@@ -164,6 +173,8 @@ __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, in
 }
 
 // The conv stack of galaxy g; the last layer writes the 1024 features to `out` (LDS or global).
+// C5 / C67: caps on the output-channel split of layer 5 and layers 6, 7 (kCSBatched / kCSOneRound)
+template <int C5, int C67>
 __device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid);
 __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, const float* __restrict__ params,
                                            float* out, float* A, float* B, int g, int tid) {
@@ -177,25 +188,26 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
         A[i * 64 + j] = m;
     }
     __syncthreads();
-    conv_layers(params, out, A, B, tid);
+    conv_layers<kCSBatched, kCSBatched>(params, out, A, B, tid);
 }
 // the four Down blocks from the pooled |H|^2 in A[64][64]
+template <int C5, int C67>
 __device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
     const float* P = params;
-#define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT)                                             \
-    conv_layer<CI, CO, S, POOL, QUAD>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid);     \
+#define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT, CMAX)                                       \
+    conv_layer<CI, CO, S, POOL, QUAD, CMAX>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid); \
     __syncthreads();                                                                             \
     SN_TRACE(3 + l);
-    GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B)   // B[4][64][64]
-    GD_SN_LAYER(1, 4, 4, 64, true, true, B, A)          // A[4][32][32]   (+ MaxPool of Down(4,8))
-    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B)   // B[8][32][32]
-    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A)          // A[8][16][16]   (+ MaxPool of Down(8,16))
-    GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B)  // B[16][16][16]
-    GD_SN_LAYER(5, 16, 16, 16, true, true, B, A)        // A[16][8][8]    (+ MaxPool of Down(16,16))
-    GD_SN_LAYER(6, 16, 16, 8, false, false, A, B)       // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
+    GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64)   // B[4][64][64]
+    GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64)          // A[4][32][32]   (+ MaxPool of Down(4,8))
+    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, 64)   // B[8][32][32]
+    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, 64)          // A[8][16][16]   (+ MaxPool of Down(8,16))
+    GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B, 64)  // B[16][16][16]
+    GD_SN_LAYER(5, 16, 16, 16, true, true, B, A, C5) // A[16][8][8]    (+ MaxPool of Down(16,16))
+    GD_SN_LAYER(6, 16, 16, 8, false, false, A, B, C67)  // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
 #undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
-    conv_layer<16, 16, 8, false>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+    conv_layer<16, 16, 8, false, false, C67>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
     SN_TRACE(10);
 }
 
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void k_subnet_features_psf(const float* _
     const int g = blockIdx.x;
     if (g >= N) return;  // uniform per block; no barrier crossed
     psf_pool(psf + (long long)g * psf_gstride, h, AB, threadIdx.x);
-    conv_layers(params, feat + (size_t)g * 1024, AB, AB + kRegionA, threadIdx.x);
+    conv_layers<kCSBatched, kCSBatched>(params, feat + (size_t)g * 1024, AB, AB + kRegionA, threadIdx.x);
 }
 
 // ---- the SubNet's MLP (models/Unrolled_ADMM.py:68-74, :85-86) over a batch of feature vectors:
@@ -437,7 +449,7 @@ __global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __res
     psf_pool(psf + (long long)g * psf_gstride, h, AB, tid);
     float* X = AB;                 // features [1024] (region A is free once layer 6 has been read)
     float* P = AB + kRegionA;      // partial sums [8][64], then h1, h2 (region B, after layer 7 read it)
-    conv_layers(params, X, AB, AB + kRegionA, tid);
+    conv_layers<kCSOneRound, kCSOneRound>(params, X, AB, AB + kRegionA, tid);
     __syncthreads();
     const float xa = alpha[(long long)g * alpha_stride];
     const float* W1 = mlp;
