@@ -50,7 +50,10 @@ __device__ unsigned long long* g_sn_trace;
 #endif
 constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #ifndef GD_SN_CS4
-#define GD_SN_CS4 64  // experiment: the same cap for layer 4 (8 -> 16 at 16^2) in the batched kernel
+#define GD_SN_CS4 4   // the same cap for layer 4 (8 -> 16 at 16^2) in the batched kernel: 400 -> 389 us
+#endif
+#ifndef GD_SN_CS23
+#define GD_SN_CS23 64  // experiment: cap for layers 2, 3 (at 32^2) in the batched kernel
 #endif
 #ifndef GD_SN_UNROLL_PX
 #define GD_SN_UNROLL_PX 2  // input channels per unrolled step: per-pixel layers
@@ -203,8 +206,8 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     SN_TRACE(3 + l);
     GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64)   // B[4][64][64]
     GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64)          // A[4][32][32]   (+ MaxPool of Down(4,8))
-    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, 64)   // B[8][32][32]
-    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, 64)          // A[8][16][16]   (+ MaxPool of Down(8,16))
+    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64))   // B[8][32][32]
+    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, (C5 < 64 ? GD_SN_CS23 : 64))          // A[8][16][16]   (+ MaxPool of Down(8,16))
     GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS4 : 64))  // B[16][16][16]
     GD_SN_LAYER(5, 16, 16, 16, true, true, B, A, C5) // A[16][8][8]    (+ MaxPool of Down(16,16))
     GD_SN_LAYER(6, 16, 16, 8, false, false, A, B, C67)  // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
