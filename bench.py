@@ -9,7 +9,11 @@ denoiser replaced by the identity so the timed region is exactly the hot path th
 ``end_to_end`` on a sample).  Inputs are synthetic (``gdeconv.synth``), weights deterministic
 (``gdeconv.weights``), all resident in HBM before timing.
 
-  python bench.py [--gpus N --steps K --warmup W]        # N>1: launched by torch.distributed.run
+  python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: under torch.distributed.run (WORLD_SIZE set) each process is one rank; without a launcher the
+process spawns the N ranks itself (``spawn_ranks``) and forwards rank 0's line.  A process group whose
+size is not N, or fewer visible GPUs than RCCL ranks, exits non-zero.
 
 Rank 0 prints ONE JSON line (value = all ranks' galaxies / max-over-ranks wall time).
 """
@@ -266,18 +270,66 @@ def cpu_baseline(args):
                       f"{done // n} passes, {t_total:.1f}s"}
 
 
+def spawn_ranks(args, argv):
+    """``--gpus N > 1`` without a launcher: start N fresh rank processes through
+    ``torch.distributed.run`` (127.0.0.1, a free port) as CHILDREN of this process - which has made no
+    GPU call (no torch.cuda.*, no engine library) and never execs - forward rank 0's JSON line to
+    stdout, and return the launcher's exit code (non-zero also when no line came back)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    print(f"[bench] --gpus {args.gpus} without WORLD_SIZE: launching {args.gpus} ranks: {' '.join(cmd)}",
+          file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print("[bench] error: the ranks exited without a result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def max_over_ranks(x, world, backend, dev):
+    """MAX of a host float over the ranks (on the device under RCCL, in host memory under gloo)."""
+    if world == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, sys.argv[1:]))
     from gdeconv import _lib
     from gdeconv.dist import init_process_group, local_device
     from gdeconv.synth import make_batch
 
     rank, world, local = init_process_group()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but the process group has {world} rank(s) "
+              f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')})", file=sys.stderr)
+        sys.exit(2)
+    backend = dist.get_backend() if world > 1 else None
+    if backend == "nccl" and torch.cuda.device_count() < world:
+        print(f"[bench] error: {world} RCCL ranks but {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+        sys.exit(2)
     dev = local_device(local)
     torch.cuda.set_device(dev)
-    backend = dist.get_backend() if world > 1 else None
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     lib = _lib.load()
@@ -344,10 +396,7 @@ def main():
         kstats = _lib.profile_collect()
         assert torch.isfinite(out).all(), "non-finite output"
 
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = max_over_ranks(t1 - t0, world, backend, dev)
     gal_s = N * world * args.steps / elapsed
 
     gather_ms, with_gather = None, None
@@ -359,7 +408,7 @@ def main():
         tg = time.perf_counter()
         gather_batch(out, N * world)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+        gather_ms = max_over_ranks(time.perf_counter() - tg, world, backend, dev) * 1e3
         # ... and overlapped: step k's gather in flight (RCCL's stream) while step k + 1 computes
         with torch.no_grad():
             dist.barrier()
@@ -373,10 +422,9 @@ def main():
                 pend = gather_batch(o_, N * world, async_op=True)
             pend.wait()
             torch.cuda.synchronize()
-            tw = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=dev)
-            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-        with_gather = {"value": N * world * args.steps / float(tw.item()), "unit": "galaxies/s",
-                       "ms_per_step": float(tw.item()) * 1e3 / args.steps,
+            tw = max_over_ranks(time.perf_counter() - tw, world, backend, dev)
+        with_gather = {"value": N * world * args.steps / tw, "unit": "galaxies/s",
+                       "ms_per_step": tw * 1e3 / args.steps,
                        "note": "each step's outputs all-gathered to every rank, overlapped with the next step"}
 
     # the same forward captured once as a hipGraph (gdeconv.graphs) and replayed: what a serving loop
@@ -396,10 +444,7 @@ def main():
             for _ in range(args.steps):
                 r = fn()
             torch.cuda.synchronize()
-            t = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
-            if world > 1:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return float(t.item()), r
+            return max_over_ranks(time.perf_counter() - t, world, backend, dev), r
 
         # eager and replayed blocks interleaved (3 rounds, medians): the same clock window for both, so
         # the comparison is not a property of which ran first on a warming / throttling chip
@@ -440,10 +485,7 @@ def main():
                 for o_, p_, a_ in it:
                     iout = model(o_, p_, a_)
                 torch.cuda.synchronize()
-                ti = torch.tensor([time.perf_counter() - ti0], dtype=torch.float64, device=dev)
-                if world > 1:
-                    dist.all_reduce(ti, op=dist.ReduceOp.MAX)
-                ti = float(ti.item())
+                ti = max_over_ranks(time.perf_counter() - ti0, world, backend, dev)
                 per_gal = (L * L + psf.shape[-1] * psf.shape[-2] + 1) * 4
                 ingest = {"value": N * world * args.steps / ti, "unit": "galaxies/s", "ms_per_step": ti * 1e3 / args.steps,
                           "bytes_per_galaxy": per_gal, "host_to_device_GBs": per_gal * N * args.steps / ti / 1e9,
@@ -527,6 +569,7 @@ def main():
                    "llh": None if rl else args.llh,
                    "parallelism": f"dp{world} (batch shards, no data-path collective"
                                   + (f"; {backend} process group, {world} ranks)" if backend else ")"),
+                   "ranks_seen": world, "backend": backend or "none",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))

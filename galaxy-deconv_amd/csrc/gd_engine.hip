@@ -2239,6 +2239,9 @@ struct PipeRes {
     hipStream_t st[kMaxPipe];
     hipEvent_t fork;
     hipEvent_t join[kMaxPipe];
+    // held from the fork record to the last join wait of one pipelined call: the fork / join events and
+    // the internal streams are per device, so concurrent callers (host threads) enqueue one at a time
+    std::mutex mu;
 };
 PipeRes g_pipe[64];
 std::mutex g_pipe_mu;
@@ -2302,6 +2305,8 @@ int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
     if (S > a.N / G) S = a.N / G;  // regions must fit the caller's workspace
     PipeRes* r = S > 1 ? pipe_res() : nullptr;
     if (!r) S = 1;
+    std::unique_lock<std::mutex> lk;
+    if (S > 1) lk = std::unique_lock<std::mutex>(r->mu);
     if (S > 1) {
         if (hipEventRecord(r->fork, st) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
         for (int i = 0; i < S; ++i)
@@ -2674,6 +2679,13 @@ void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     }
 }
 }  // namespace
+
+int gd_admm_state_layout(int H, int W, int llh) {
+    if (!gd_supported_size(H, W)) return GD_ERR_UNSUPPORTED;
+    if (llh == GD_LLH_GAUSSIAN) return 1;
+    if (llh != GD_LLH_POISSON) return GD_ERR_ARG;
+    return pois_two_pass(H, W, llh) ? 2 : 3;
+}
 
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,

@@ -35,6 +35,7 @@ SIGNATURES = {
     "gd_rfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_admm_state_bytes": (_SZ, [_I, _I, _I, _I]),
+    "gd_admm_state_layout": (_I, [_I, _I, _I]),
     "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P]),
     "gd_admm_iter": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P,
                           _P]),

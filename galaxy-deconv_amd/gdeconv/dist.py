@@ -37,6 +37,9 @@ def init_process_group(backend=None):
     if backend is None:
         backend = os.environ.get("GD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
+        if torch.cuda.device_count() <= local:
+            raise RuntimeError(f"RCCL rank {rank} (local rank {local}) but {torch.cuda.device_count()} visible "
+                               "GPU(s): RCCL needs one GPU per rank (GD_DIST_BACKEND=gloo rehearses on fewer)")
         torch.cuda.set_device(local)
     dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
@@ -77,6 +80,11 @@ def gather_batch(local, N, chunk_bytes=256 << 20, async_op=False):
     and placed with one strided copy, so the xGMI transfers of chunk c + 1 overlap the placement of
     chunk c; uneven shards are padded to the largest slice.  ``async_op=True`` returns a
     ``PendingGather`` instead (overlap with the next batch's compute; see its ``wait``)."""
+    if local.is_cuda and dist.get_backend() == "gloo":
+        # gloo has no device all-gather: gather host copies, place the result on the device (the
+        # multi-rank rehearsal on one GPU; RCCL's path below is the product path)
+        out = gather_batch(local.cpu(), N, chunk_bytes).to(local.device)
+        return PendingGather(out, [], []) if async_op else out
     world = dist.get_world_size()
     rank = dist.get_rank()
     sizes = [shard_range(N, r, world) for r in range(world)]

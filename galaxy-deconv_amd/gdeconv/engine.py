@@ -260,6 +260,12 @@ def tikhonov(y, psf, alpha, lam, ltl=None):
     return out
 
 
+def mlp_supported(n_out):
+    """True if the engine's SubNet MLP kernels take ``n_out`` outputs (1 .. 64); larger MLPs (more than
+    32 ADMM iterations) run the feature kernel and the PyTorch MLP."""
+    return _lib.load().gd_subnet_mlp_param_count(int(n_out)) > 0
+
+
 def subnet_rhos(otf128, params, mlp_params, alpha, n_out):
     """The whole SubNet forward (``k_subnet_features`` + the batched ``k_subnet_mlp``: MLP, Softplus,
     + 1e-6) -> [N, n_out]; ``mlp_params`` packed (transposed weights) as documented in include/gdeconv.h,
@@ -489,6 +495,7 @@ class ADMMState:
                 self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
                 self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.state.data_ptr(),
                 self.zin.data_ptr(), ws.data_ptr(), _stream(self.dev)), "gd_admm_init")
+        self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
         self.iter = 0
 
     def step(self, z, rho1, rho2, rho2_next, out=None):
@@ -498,6 +505,9 @@ class ADMMState:
         z = z.float().contiguous()
         if z.shape != self.y.shape:
             raise ValueError(f"denoiser returned {tuple(z.shape)}, expected {tuple(self.y.shape)}")
+        if self.lib.gd_admm_state_layout(self.H, self.W, self.llh) != self.layout:
+            raise _lib.EngineError("the ADMM state layout changed since init (gd_set_fused_iteration toggled "
+                                   "between gd_admm_init and gd_admm_iter)")
         last = rho2_next is None
         dst = out if last else self.zin
         r1, r1s = rho1
@@ -517,4 +527,5 @@ class ADMMState:
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
            "tikhonov", "filter_power", "filter_power_taps", "GaussXState", "gx_x_update",
-           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos", "subnet_rhos_psf"]
+           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos", "subnet_rhos_psf",
+           "mlp_supported"]

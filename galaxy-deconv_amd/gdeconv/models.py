@@ -18,10 +18,13 @@ hard-codes ``cuda:0``, ``models/Unrolled_ADMM.py:178``), the OTF is computed on 
 reference builds it on the CPU every forward, ``utils/utils_torch.py:81``), CPU tensors are
 rejected (no CPU path), unsupported reference variants raise instead of misbehaving
 (``PnP=False``: the reference's l1 ``Z_Update`` call uses an undefined ``lam``, ``:208``), and
-``Unrolled_ADMM`` is inference-only: its forward raises under autograd when a parameter requires
-grad (the engine writes through raw pointers, so no graph would reach ``self.Z`` / ``self.init``;
-the differentiable variant is ``UnrolledADMMGaussian``, whose X update has a HIP backward).
+``Unrolled_ADMM`` is inference-only: in training mode its forward raises under autograd when a
+parameter requires grad (the engine writes through raw pointers, so no graph would reach ``self.Z`` /
+``self.init``; the differentiable variant is ``UnrolledADMMGaussian``, whose X update has a HIP
+backward); in eval mode it runs under ``torch.no_grad()`` and returns an output without a graph.
 """
+import warnings
+
 import torch
 import torch.nn as nn
 
@@ -69,9 +72,24 @@ class Unrolled_ADMM(nn.Module):
 
     def forward(self, y, kernel, alpha):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "Unrolled_ADMM on the HIP engine is inference-only (wrap the call in torch.no_grad() or "
-                "freeze the parameters); train UnrolledADMMGaussian, whose X update has a HIP backward")
+            if self.training:
+                raise NotImplementedError(
+                    "Unrolled_ADMM on the HIP engine is inference-only (call .eval(), wrap the call in "
+                    "torch.no_grad() or freeze the parameters); train UnrolledADMMGaussian, whose X update "
+                    "has a HIP backward")
+            # eval mode with grad enabled (e.g. figures/grid_plot.ipynb calls the model and .detach()es):
+            # the output carries no graph, as documented above
+            if not Unrolled_ADMM._warned_grad:
+                Unrolled_ADMM._warned_grad = True
+                warnings.warn("Unrolled_ADMM (HIP engine) runs inference under torch.no_grad(): the output "
+                              "does not require grad", stacklevel=2)
+            with torch.no_grad():
+                return self._forward(y, kernel, alpha)
+        return self._forward(y, kernel, alpha)
+
+    _warned_grad = False
+
+    def _forward(self, y, kernel, alpha):
         N = y.shape[0]
         rho1_iters, rho2_iters = self.rhos(kernel, alpha)
         st = engine.ADMMState(y, kernel, alpha, self.llh)

@@ -249,7 +249,8 @@ class SubNet(nn.Module):
             # MLP stays in PyTorch after k_subnet_features so its parameters get gradients)
             from . import engine
             dev = kernel.device
-            if not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
+            mlp_ok = engine.mlp_supported(self.n_out)  # k_subnet_mlp: n_out <= 64 (kMaxOut)
+            if mlp_ok and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
                 if h <= 64:  # |FFT2(pad128(psf))|^2 inside the feature kernel (no OTF128 pre-pass)
                     out = engine.subnet_rhos_psf(kernel, self._packed_params().to(dev), self._packed_mlp().to(dev),
                                                  alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)

@@ -94,6 +94,12 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
  *               denoiser input x + u1 -> zin_or_out; last != 0 -> zin_or_out = x (times alpha for
  *               Poisson).  z may alias zin_or_out (identity denoiser). */
 size_t gd_admm_state_bytes(int N, int H, int W, int llh);
+/* Which state layout gd_admm_init would write NOW for (H, W, llh): 1 = Gaussian spectral, 2 = Poisson
+ * in two whole-galaxy passes (256^2 with a fused iteration: [|H|^2 | H | U1 | W~ | X] + w), 3 = Poisson
+ * three-kernel ([otf | u1 | w]); negative = unsupported.  The Poisson layout follows
+ * gd_set_fused_iteration, so a caller records it at init and checks it before each gd_admm_iter (a
+ * toggle in between would bind a different layout than the init wrote). */
+int gd_admm_state_layout(int H, int W, int llh);
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
                  int llh, int N, int H, int W, void* state, float* zin, void* ws, void* stream);

@@ -52,6 +52,47 @@ def test_two_streams_bit_identical_to_serial(dev):
         assert torch.equal(res[("c", rep)], serial[2])
 
 
+def test_two_host_threads_pipelined_calls(dev):
+    """Two host threads issuing chunked (Infinity-Cache pipelined) operations at once, each on its own
+    stream: the per-device fork / join events and internal streams are taken under a lock per call, so
+    every result equals the serial one bit for bit."""
+    import threading
+    from gdeconv import _lib, engine
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    old = lib.gd_set_chunk_bytes(8 << 20)     # 15 galaxies of 256^2 per chunk -> many chunks per call
+    try:
+        obs, psf, alpha, _ = make_batch(40, 256, seed=31, device=dev)
+        serial_w = engine.wiener(obs, psf, alpha)
+        serial_c = engine.conv_half(engine.psf_to_otf_half(psf, 40, 256, 256), obs)
+        torch.cuda.synchronize()
+        res, errs = {}, []
+
+        def work(tag):
+            try:
+                s = torch.cuda.Stream(dev)
+                with torch.cuda.stream(s):
+                    for rep in range(4):
+                        res[(tag, "w", rep)] = engine.wiener(obs, psf, alpha)
+                        res[(tag, "c", rep)] = engine.conv_half(engine.psf_to_otf_half(psf, 40, 256, 256), obs)
+                s.synchronize()
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        ts = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert not errs, errs
+        for t in range(2):
+            for rep in range(4):
+                assert torch.equal(res[(t, "w", rep)], serial_w)
+                assert torch.equal(res[(t, "c", rep)], serial_c)
+    finally:
+        lib.gd_set_chunk_bytes(old)
+
+
 def test_conv_fft_batch_shared_otf_broadcasts(dev):
     """conv_fft_batch(H, x) with ONE [1,1,H,W] OTF for N images (the reference's fftn(x) * H broadcast,
     utils/utils_torch.py:46-50): equal to the expanded per-galaxy OTF bit for bit, and to the oracle."""

@@ -67,3 +67,37 @@ def test_two_ranks_drive_the_engine():
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def _bench(argv, env_extra, timeout=600):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *argv], capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_spawns_its_ranks():
+    """``bench.py --gpus 2`` with no launcher starts its two ranks itself (gloo rehearsal on one GPU)
+    and prints ONE line for the 2-rank job, with the all-gather timings of the multi-rank path."""
+    import json
+    r = _bench(["--gpus", "2", "--batch", "64", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ingest",
+                "--no-cpu-baseline"], {"GD_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["ranks_seen"] == 2 and rec["config"]["backend"] == "gloo"
+    assert rec["config"]["global_batch"] == 128 and rec["value"] > 0
+    assert rec["gather_ms"] > 0 and rec["with_gather"]["value"] > 0
+    assert rec["graphed"]["bit_identical_to_eager"]
+
+
+def test_bench_refuses_more_rccl_ranks_than_gpus():
+    """RCCL needs one GPU per rank: ``--gpus N`` beyond the visible GPUs exits non-zero (no 1-rank line)."""
+    n = torch.cuda.device_count() + 1
+    r = _bench(["--gpus", str(n), "--batch", "8", "--steps", "1", "--warmup", "0", "--no-e2e", "--no-ingest",
+                "--no-cpu-baseline", "--no-graph"], {"GD_DIST_BACKEND": "nccl"}, timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -508,6 +508,46 @@ def test_subnet_rhos_from_psf_matches_otf_path(dev, h):
     assert nerr(a.cpu(), ref.cpu()) < 1e-5
 
 
+def test_subnet_more_than_32_iterations(dev):
+    """n_iters = 40 (80 MLP outputs, beyond the engine MLP's 64): the feature kernel + the PyTorch MLP,
+    against the PyTorch SubNet (fold off)."""
+    from gdeconv.nets import SubNet
+    from gdeconv.synth import make_batch
+    from gdeconv.weights import make_state_dict
+    net = SubNet(40)
+    net.load_state_dict(make_state_dict(net, 17))
+    net = net.to(dev).eval()
+    N = 9
+    _, psf, alpha, _ = make_batch(N, 64, h=48, seed=18)
+    psf, alpha = psf.to(dev), alpha.to(dev)
+    with torch.no_grad():
+        r1, r2 = net(psf, alpha)
+        net.set_fold_bn(False)
+        r1_ref, r2_ref = net(psf, alpha)
+        net.set_fold_bn(True)
+    assert r1.shape == (N, 1, 1, 40) and r2.shape == (N, 1, 1, 40)
+    assert nerr(r1.reshape(N, -1).cpu(), r1_ref.reshape(N, -1).cpu()) < 1e-5
+    assert nerr(r2.reshape(N, -1).cpu(), r2_ref.reshape(N, -1).cpu()) < 1e-5
+
+
+def test_eval_mode_forward_with_grad_enabled(dev):
+    """figures/grid_plot.ipynb calls an eval-mode Unrolled_ADMM without torch.no_grad() and .detach()es
+    the result: the drop-in runs it under no_grad, with the same output."""
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.synth import make_batch
+    from gdeconv.weights import make_state_dict
+    m = Unrolled_ADMM(n_iters=2, llh="Gaussian")
+    m.load_state_dict(make_state_dict(m, 3))
+    m = m.to(dev).eval()
+    m.Z = torch.nn.Identity()   # engine + SubNet only (MIOpen's first-call algorithm search is not bitwise stable)
+    obs, psf, alpha, _ = make_batch(3, 48, seed=4, device=dev)
+    out = m(obs, psf, alpha)
+    assert not out.requires_grad
+    with torch.no_grad():
+        ref = m(obs, psf, alpha)
+    assert torch.equal(out.detach(), ref)
+
+
 # ------------------------------------------------------------------ Infinity-Cache pipelining
 def test_pipelined_chunks_bit_identical(dev):
     """Chunked multi-stream execution (here 9 galaxies per chunk on 3 streams, incl. a ragged last

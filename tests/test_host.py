@@ -6,7 +6,9 @@ import os
 import pytest
 import torch
 
-from conftest import GOLDEN
+import sys
+
+from conftest import GOLDEN, ROOT
 
 
 def test_state_dict_keys_match_reference():
@@ -48,6 +50,12 @@ def test_unrolled_admm_is_inference_only():
     m = Unrolled_ADMM(n_iters=1, llh="Gaussian")
     x = torch.zeros(1, 1, 48, 48)
     with pytest.raises(NotImplementedError, match="inference-only"):
+        m(x, torch.zeros(1, 1, 48, 48), torch.ones(1))
+    # eval mode with grad enabled (figures/grid_plot.ipynb) runs under no_grad: on CPU tensors it gets as
+    # far as the engine's device check
+    m.eval()
+    with pytest.warns(UserWarning, match="no_grad"), pytest.raises(ValueError, match="ROCm"):
+        Unrolled_ADMM._warned_grad = False
         m(x, torch.zeros(1, 1, 48, 48), torch.ones(1))
 
 
@@ -188,3 +196,13 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd="/tmp", capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
+def test_bench_rejects_world_size_mismatch():
+    """A process group whose size is not --gpus exits non-zero before any GPU work (no mislabelled line)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "--gpus 2" in r.stderr and not r.stdout.strip()
