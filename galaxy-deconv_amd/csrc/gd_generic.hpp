@@ -7,8 +7,8 @@
 // on a line FFT planned at run time:
 //
 //  * Stockham autosort, mixed radix: n = 4^a 2^b 3^c 5^d p1 p2 ... (radix 2, 3, 4, 5 as explicit butterflies,
-//    any other prime factor as a direct DFT of that length), all lines of a workgroup transformed in
-//    LDS, ping-pong between two line buffers, one barrier per stage;
+//    any other prime factor as a symmetric odd-prime DFT stage, odd_prime_stage), all lines of a workgroup
+//    transformed in LDS, ping-pong between two line buffers, one barrier per stage;
 //  * twiddles W_n^k = exp(-2 pi i k / n) for k < n computed per workgroup in double (sincospi) and
 //    rounded once into an LDS table - no device-side plan buffers, so the C ABI keeps its "no internal
 //    allocation, graph-capturable" contract;
@@ -81,6 +81,74 @@ __device__ __forceinline__ float2 twv(const float2* tw, int e, bool inv) {
     return inv ? make_float2(w.x, -w.y) : w;
 }
 
+// A Stockham stage of odd prime radix r >= 7 (butterfly i of each line reads x[i + t m], t < r, and
+// writes y[(i - i mod p) r + i mod p + q p]), as the symmetric form of the DFT: with the stage twiddles
+// applied, a_t = x_t W_n^{t e1}, and b_t = a_t + a_{r-t}, d_t = a_t - a_{r-t} (t = 1 .. h = (r-1)/2),
+//     X_0 = a_0 + sum_t b_t,   X_q, X_{r-q} = A_q -+ i B_q  (forward; inverse +-),
+//     A_q = a_0 + sum_t b_t cos(2 pi q t / r),   B_q = sum_t d_t sin(2 pi q t / r).
+// h^2 real-coefficient terms per butterfly instead of r^2 complex ones, and every output a sum of h terms,
+// split over two accumulators: ~1/4 of the FMAs of a direct DFT and ~3x less rounding growth (a direct
+// DFT of 61 or 97 points was 2.4-3.4x further from fp64 than the reference's FFT,
+// tests/test_gpu_pixel_parity.py).  Two phases, both spread over the workgroup: the (butterfly, pair)
+// items form b_t, d_t in place (each butterfly owns its r inputs), then the (butterfly, q) items sum.
+__device__ void odd_prime_stage(float2* x, float2* y, int n, int r, int m, int p, int ts, const float2* tw, int nl,
+                                bool inv) {
+    const int h = (r - 1) >> 1;
+    for (int idx = threadIdx.x; idx < nl * m * h; idx += blockDim.x) {
+        const int bi = idx / h, t = idx - bi * h + 1;
+        const int line = bi / m, i = bi - line * m;
+        const int e1 = (i % p) * ts;  // < m: t e1 < n
+        float2* xs = x + line * n + i;
+        float2 at = xs[t * m], ar = xs[(r - t) * m];
+        if (e1) {
+            at = cmul(at, twv(tw, t * e1, inv));
+            ar = cmul(ar, twv(tw, (r - t) * e1, inv));
+        }
+        xs[t * m] = cadd(at, ar);
+        xs[(r - t) * m] = csub(at, ar);
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nl * m * (h + 1); idx += blockDim.x) {
+        const int bi = idx / (h + 1), q = idx - bi * (h + 1);
+        const int line = bi / m, i = bi - line * m;
+        const int k = i % p;
+        const float2* xs = x + line * n + i;
+        float2* ys = y + line * n + (i - k) * r + k;
+        const float2 a0 = xs[0];
+        if (q == 0) {
+            float2 s0 = a0, s1 = make_float2(0.f, 0.f);
+            for (int t = 1; t <= h; t += 2) {
+                s0 = cadd(s0, xs[t * m]);
+                if (t + 1 <= h) s1 = cadd(s1, xs[(t + 1) * m]);
+            }
+            ys[0] = cadd(s0, s1);
+            continue;
+        }
+        float2 A0 = a0, A1 = make_float2(0.f, 0.f), B0 = A1, B1 = A1;
+        const int step = q * m;  // W_r^{q t} = W_n^{(q t mod r) m}
+        int e = 0;
+        for (int t = 1; t <= h; ++t) {
+            e += step;
+            if (e >= n) e -= n;
+            const float2 w = tw[e];          // (cos, -sin) of 2 pi (q t mod r) / r
+            const float c = w.x, sn = -w.y;
+            const float2 b = xs[t * m], d = xs[(r - t) * m];
+            if (t & 1) {
+                A0 = make_float2(fmaf(b.x, c, A0.x), fmaf(b.y, c, A0.y));
+                B0 = make_float2(fmaf(d.x, sn, B0.x), fmaf(d.y, sn, B0.y));
+            } else {
+                A1 = make_float2(fmaf(b.x, c, A1.x), fmaf(b.y, c, A1.y));
+                B1 = make_float2(fmaf(d.x, sn, B1.x), fmaf(d.y, sn, B1.y));
+            }
+        }
+        const float2 A = cadd(A0, A1), B = cadd(B0, B1);
+        // forward X_q = A - i B, X_{r-q} = A + i B (inverse: the other way round)
+        const float2 mi = make_float2(A.x + B.y, A.y - B.x), pl = make_float2(A.x - B.y, A.y + B.x);
+        ys[q * p] = inv ? pl : mi;
+        ys[(r - q) * p] = inv ? mi : pl;
+    }
+}
+
 // nl lines of length ax.n, contiguous in x ([line][n]); y is scratch of the same size.  Returns the
 // buffer holding the result (x or y).  Stage with radix r after p points combined: butterfly i < n/r
 // reads x[i + q n/r], twiddles by W_{p r}^{q (i mod p)}, DFT_r, writes y[(i - i mod p) r + i mod p + q p].
@@ -89,70 +157,57 @@ __device__ float2* fft_lines(float2* x, float2* y, const Axis& ax, const float2*
     int p = 1;
     for (int s = 0; s < ax.ns; ++s) {
         const int r = ax.r[s], m = n / r, ts = m / p;
-        for (int idx = threadIdx.x; idx < nl * m; idx += blockDim.x) {
-            const int line = idx / m, i = idx - line * m;
-            const int k = i % p;
-            const float2* xs = x + line * n + i;
-            float2* ys = y + line * n + (i - k) * r + k;
-            const int e1 = k * ts;  // < n / r
-            if (r == 2) {
-                const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv));
-                ys[0] = cadd(a0, a1);
-                ys[p] = csub(a0, a1);
-            } else if (r == 4) {
-                const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv)),
-                             a3 = cmul(xs[3 * m], twv(tw, 3 * e1, inv));
-                const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3);
-                const float2 d = csub(a1, a3);
-                const float2 t3 = inv ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);  // (a1 - a3) (-+i)
-                ys[0] = cadd(t0, t2);
-                ys[p] = cadd(t1, t3);
-                ys[2 * p] = csub(t0, t2);
-                ys[3 * p] = csub(t1, t3);
-            } else if (r == 3) {
-                const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv));
-                const float2 sm = cadd(a1, a2), df = csub(a1, a2);
-                const float2 t = make_float2(a0.x - 0.5f * sm.x, a0.y - 0.5f * sm.y);
-                const float c3 = 0.866025403784438646763723f;                 // sin(2 pi / 3)
-                // forward: W = -1/2 - i sqrt(3)/2;  -i c3 (a1 - a2) for X1, +i c3 (a1 - a2) for X2
-                const float2 u = inv ? make_float2(-c3 * df.y, c3 * df.x) : make_float2(c3 * df.y, -c3 * df.x);
-                ys[0] = cadd(a0, sm);
-                ys[p] = cadd(t, u);
-                ys[2 * p] = csub(t, u);
-            } else if (r == 5) {
-                const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv)),
-                             a3 = cmul(xs[3 * m], twv(tw, 3 * e1, inv)), a4 = cmul(xs[4 * m], twv(tw, 4 * e1, inv));
-                const float c1 = 0.309016994374947424102f, c2 = -0.809016994374947424102f;  // cos(2pi/5), cos(4pi/5)
-                const float s1 = 0.951056516295153572116f, s2 = 0.587785252292473129169f;   // sin(2pi/5), sin(4pi/5)
-                const float2 b1 = cadd(a1, a4), b2 = cadd(a2, a3), d1 = csub(a1, a4), d2 = csub(a2, a3);
-                const float2 t1 = make_float2(a0.x + c1 * b1.x + c2 * b2.x, a0.y + c1 * b1.y + c2 * b2.y);
-                const float2 t2 = make_float2(a0.x + c2 * b1.x + c1 * b2.x, a0.y + c2 * b1.y + c1 * b2.y);
-                const float2 u1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
-                const float2 u2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
-                // forward: X1 = t1 - i u1, X4 = t1 + i u1, X2 = t2 - i u2, X3 = t2 + i u2 (inverse: i -> -i)
-                const float2 iu1 = inv ? make_float2(-u1.y, u1.x) : make_float2(u1.y, -u1.x);
-                const float2 iu2 = inv ? make_float2(-u2.y, u2.x) : make_float2(u2.y, -u2.x);
-                ys[0] = cadd(a0, cadd(b1, b2));
-                ys[p] = cadd(t1, iu1);
-                ys[2 * p] = cadd(t2, iu2);
-                ys[3 * p] = csub(t2, iu2);
-                ys[4 * p] = csub(t1, iu1);
-            } else {
-                // direct DFT of prime length r: X_q = sum_t x_t W_n^{t (e1 + q m)}, the twiddle index
-                // advanced by step (< n) and reduced by one compare per term
-                for (int q = 0; q < r; ++q) {
-                    float2 acc = make_float2(0.f, 0.f);
-                    const int step = e1 + q * m;
-                    int e = 0;
-                    for (int t = 0; t < r; ++t) {
-                        const float2 w = twv(tw, e, inv);
-                        const float2 v = xs[t * m];
-                        acc.x = fmaf(v.x, w.x, fmaf(-v.y, w.y, acc.x));
-                        acc.y = fmaf(v.x, w.y, fmaf(v.y, w.x, acc.y));
-                        e += step;
-                        if (e >= n) e -= n;
-                    }
-                    ys[q * p] = acc;
+        if (r > 5) {
+            odd_prime_stage(x, y, n, r, m, p, ts, tw, nl, inv);
+        } else {
+            for (int idx = threadIdx.x; idx < nl * m; idx += blockDim.x) {
+                const int line = idx / m, i = idx - line * m;
+                const int k = i % p;
+                const float2* xs = x + line * n + i;
+                float2* ys = y + line * n + (i - k) * r + k;
+                const int e1 = k * ts;  // < n / r
+                if (r == 2) {
+                    const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv));
+                    ys[0] = cadd(a0, a1);
+                    ys[p] = csub(a0, a1);
+                } else if (r == 4) {
+                    const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv)),
+                                 a3 = cmul(xs[3 * m], twv(tw, 3 * e1, inv));
+                    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3);
+                    const float2 d = csub(a1, a3);
+                    const float2 t3 = inv ? make_float2(-d.y, d.x) : make_float2(d.y, -d.x);  // (a1 - a3) (-+i)
+                    ys[0] = cadd(t0, t2);
+                    ys[p] = cadd(t1, t3);
+                    ys[2 * p] = csub(t0, t2);
+                    ys[3 * p] = csub(t1, t3);
+                } else if (r == 3) {
+                    const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv));
+                    const float2 sm = cadd(a1, a2), df = csub(a1, a2);
+                    const float2 t = make_float2(a0.x - 0.5f * sm.x, a0.y - 0.5f * sm.y);
+                    const float c3 = 0.866025403784438646763723f;                 // sin(2 pi / 3)
+                    // forward: W = -1/2 - i sqrt(3)/2;  -i c3 (a1 - a2) for X1, +i c3 (a1 - a2) for X2
+                    const float2 u = inv ? make_float2(-c3 * df.y, c3 * df.x) : make_float2(c3 * df.y, -c3 * df.x);
+                    ys[0] = cadd(a0, sm);
+                    ys[p] = cadd(t, u);
+                    ys[2 * p] = csub(t, u);
+                } else {  // r == 5
+                    const float2 a0 = xs[0], a1 = cmul(xs[m], twv(tw, e1, inv)), a2 = cmul(xs[2 * m], twv(tw, 2 * e1, inv)),
+                                 a3 = cmul(xs[3 * m], twv(tw, 3 * e1, inv)), a4 = cmul(xs[4 * m], twv(tw, 4 * e1, inv));
+                    const float c1 = 0.309016994374947424102f, c2 = -0.809016994374947424102f;  // cos(2pi/5), cos(4pi/5)
+                    const float s1 = 0.951056516295153572116f, s2 = 0.587785252292473129169f;   // sin(2pi/5), sin(4pi/5)
+                    const float2 b1 = cadd(a1, a4), b2 = cadd(a2, a3), d1 = csub(a1, a4), d2 = csub(a2, a3);
+                    const float2 t1 = make_float2(a0.x + c1 * b1.x + c2 * b2.x, a0.y + c1 * b1.y + c2 * b2.y);
+                    const float2 t2 = make_float2(a0.x + c2 * b1.x + c1 * b2.x, a0.y + c2 * b1.y + c1 * b2.y);
+                    const float2 u1 = make_float2(s1 * d1.x + s2 * d2.x, s1 * d1.y + s2 * d2.y);
+                    const float2 u2 = make_float2(s2 * d1.x - s1 * d2.x, s2 * d1.y - s1 * d2.y);
+                    // forward: X1 = t1 - i u1, X4 = t1 + i u1, X2 = t2 - i u2, X3 = t2 + i u2 (inverse: i -> -i)
+                    const float2 iu1 = inv ? make_float2(-u1.y, u1.x) : make_float2(u1.y, -u1.x);
+                    const float2 iu2 = inv ? make_float2(-u2.y, u2.x) : make_float2(u2.y, -u2.x);
+                    ys[0] = cadd(a0, cadd(b1, b2));
+                    ys[p] = cadd(t1, iu1);
+                    ys[2 * p] = cadd(t2, iu2);
+                    ys[3 * p] = csub(t2, iu2);
+                    ys[4 * p] = csub(t1, iu1);
                 }
             }
         }

@@ -46,7 +46,10 @@ def _require_device(*ts):
 @contextlib.contextmanager
 def _on(device):
     """Make ``device`` current for the duration of one engine call (the C side picks its internal
-    pipeline streams by the current HIP device)."""
+    pipeline streams by the current HIP device); no device switch when it already is."""
+    if device.index is None or torch.cuda.current_device() == device.index:
+        yield
+        return
     with torch.cuda.device(device):
         yield
 
@@ -260,10 +263,27 @@ def tikhonov(y, psf, alpha, lam, ltl=None):
     return out
 
 
+_MLP_COUNT = {}
+
+
+def _mlp_param_count(n_out):
+    c = _MLP_COUNT.get(n_out)
+    if c is None:
+        c = _MLP_COUNT[n_out] = int(_lib.load().gd_subnet_mlp_param_count(int(n_out)))
+    return c
+
+
+def _subnet_param_count():
+    c = _MLP_COUNT.get("conv")
+    if c is None:
+        c = _MLP_COUNT["conv"] = int(_lib.load().gd_subnet_param_count())
+    return c
+
+
 def mlp_supported(n_out):
     """True if the engine's SubNet MLP kernels take ``n_out`` outputs (1 .. 64); larger MLPs (more than
     32 ADMM iterations) run the feature kernel and the PyTorch MLP."""
-    return _lib.load().gd_subnet_mlp_param_count(int(n_out)) > 0
+    return _mlp_param_count(n_out) > 0
 
 
 def subnet_rhos(otf128, params, mlp_params, alpha, n_out):
@@ -275,9 +295,9 @@ def subnet_rhos(otf128, params, mlp_params, alpha, n_out):
     N = otf128.shape[0]
     if tuple(otf128.shape[1:]) != (65, 128) or otf128.dtype != torch.complex64:
         raise ValueError("otf128 must be complex64 [N, 65, 128]")
-    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+    if params.numel() != _subnet_param_count() or params.dtype != torch.float32:
         raise ValueError("bad SubNet parameter pack")
-    if mlp_params.numel() != lib.gd_subnet_mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
+    if mlp_params.numel() != _mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
         raise ValueError("bad SubNet MLP parameter pack")
     al = alpha.reshape(-1).float().contiguous()
     if al.numel() not in (1, N):
@@ -302,9 +322,9 @@ def subnet_rhos_psf(psf, params, mlp_params, alpha, n_out):
     h = k.shape[2]
     if k.shape[3] != h or h % 2 or h > 64:
         raise ValueError("subnet_rhos_psf needs an even square PSF of side <= 64")
-    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+    if params.numel() != _subnet_param_count() or params.dtype != torch.float32:
         raise ValueError("bad SubNet parameter pack")
-    if mlp_params.numel() != lib.gd_subnet_mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
+    if mlp_params.numel() != _mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32:
         raise ValueError("bad SubNet MLP parameter pack")
     al = alpha.reshape(-1).float().contiguous()
     if al.numel() not in (1, N):
@@ -327,7 +347,7 @@ def subnet_features(otf128, params):
     N = otf128.shape[0]
     if tuple(otf128.shape[1:]) != (65, 128) or otf128.dtype != torch.complex64:
         raise ValueError("otf128 must be complex64 [N, 65, 128]")
-    if params.numel() != lib.gd_subnet_param_count() or params.dtype != torch.float32:
+    if params.numel() != _subnet_param_count() or params.dtype != torch.float32:
         raise ValueError("bad SubNet parameter pack")
     otf128 = otf128.contiguous()
     with _on(dev):
@@ -452,10 +472,63 @@ def gx_x_update(st, z, u, rho):
     return _XUpdateGaussianFn.apply(z, u, rho, st)
 
 
+class RhoSchedule:
+    """Per-iteration (device pointer, galaxy stride) pairs of a penalty schedule, computed once per
+    forward: a [N', 1, 1, n] SubNet output (N' = N, or 1 = shared; any view whose last dim is unit
+    stride, e.g. the rho1 / rho2 halves of the MLP output) or an [n] parameter.  No per-iteration slicing
+    or tensor creation: iteration ``it`` is ``base + 4 it`` (models/Unrolled_ADMM.py:201-206 index
+    ``rho1_iters[:, :, :, n]``)."""
+
+    __slots__ = ("t", "base", "gs", "n")
+
+    def __init__(self, rho_iters, N, device):
+        t = rho_iters.detach()
+        if t.dtype != torch.float32:
+            t = t.float()
+        if t.device != torch.device(device):
+            raise ValueError(f"rho schedule is on {t.device}, the inputs on {device}")
+        if t.dim() == 4:
+            t = t.reshape(t.shape[0], t.shape[-1]) if t.shape[1] == 1 and t.shape[2] == 1 else None
+            if t is None:
+                raise ValueError("rho schedule must be [N,1,1,n]")
+            if t.stride(1) != 1:
+                t = t.contiguous()
+            if t.shape[0] not in (1, N):
+                raise ValueError(f"rho schedule batch must be 1 or N={N}")
+            self.gs = t.stride(0) if (t.shape[0] == N and N > 1) else 0
+            self.n = t.shape[1]
+        elif t.dim() == 1:
+            t = t.contiguous()
+            self.gs, self.n = 0, t.shape[0]
+        else:
+            raise ValueError("rho schedule must be [N,1,1,n] or [n]")
+        self.t, self.base = t, t.data_ptr()
+
+    def __getitem__(self, it):
+        if not 0 <= it < self.n:
+            raise IndexError(f"iteration {it} outside the schedule of {self.n}")
+        return self.base + 4 * it, self.gs
+
+
+def _scalar_arg(x, dev):
+    """(pointer, stride) from a (tensor | device pointer, stride) pair."""
+    p, s = x
+    if torch.is_tensor(p):
+        if p.device != dev:
+            raise ValueError(f"per-galaxy scalar on {p.device}, the inputs on {dev}")
+        if p.dtype != torch.float32:
+            raise ValueError("per-galaxy scalars must be fp32")
+        return p.data_ptr(), s
+    return int(p), s
+
+
 class ADMMState:
     """Device state of one unrolled-ADMM forward: the engine's opaque state buffer (OTF + u1 and
-    v - u2, spectral for llh='Gaussian', spatial for 'Poisson') and ``zin``, the next denoiser
-    input (x + u1)."""
+    v - u2, spectral for llh='Gaussian', spatial for 'Poisson'), ``zin``, the next denoiser input
+    (x + u1), and the call scratch.  Everything is allocated once at construction (on the current
+    stream of the inputs' device) and reused by ``init`` and every ``step``, which are stream-ordered
+    on that stream like the state itself; a step validates only what changes per call (z, the output),
+    so the host cost per iteration is one ctypes call (the 48^2 LSST batch is host-launch-bound)."""
 
     def __init__(self, y, psf, alpha, llh):
         self.dev = _require_device(y, psf, alpha)
@@ -473,6 +546,11 @@ class ADMMState:
             self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
             self.state = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
             self.zin = torch.empty_like(self.y)
+            self.ws = workspace(self.N, self.H, self.W, self.dev)
+        self._fixed = (self.y.data_ptr(), self.alpha.data_ptr(), self.alpha_s, self.state.data_ptr(),
+                       self.ws.data_ptr())
+        self._dev_index = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        self.layout = None
         self.iter = 0
 
     @property
@@ -485,47 +563,58 @@ class ADMMState:
         return self.state[: self.N * K * self.H * 8].view(torch.complex64).view(self.N, K, self.H)
 
     def init(self, rho2_first):
-        """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; rho2_first = (tensor, stride)."""
-        r2, r2s = rho2_first
-        _require_device(r2, self.y)
+        """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; ``rho2_first`` = (tensor or
+        device pointer, stride)."""
+        r2, r2s = _scalar_arg(rho2_first, self.dev)
         k = self.psf
+        yp, ap, as_, sp, wp = self._fixed
         with _on(self.dev):
-            ws = workspace(self.N, self.H, self.W, self.dev)
             _lib.check(self.lib.gd_admm_init(
-                self.y.data_ptr(), k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], self.alpha.data_ptr(),
-                self.alpha_s, r2.data_ptr(), r2s, self.llh, self.N, self.H, self.W, self.state.data_ptr(),
-                self.zin.data_ptr(), ws.data_ptr(), _stream(self.dev)), "gd_admm_init")
+                yp, k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], ap, as_, r2, r2s, self.llh, self.N, self.H,
+                self.W, sp, self.zin.data_ptr(), wp, _stream(self.dev)), "gd_admm_init")
         self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
         self.iter = 0
 
     def step(self, z, rho1, rho2, rho2_next, out=None):
         """One loop body (models/Unrolled_ADMM.py:207-213) after the denoiser returned ``z``.
-        ``rho*`` are (tensor, stride) views; ``rho2_next`` None marks the last iteration, whose x
-        (times alpha for Poisson) goes to ``out``."""
-        z = z.float().contiguous()
+        ``rho*`` are (tensor or device pointer, stride) pairs (``RhoSchedule`` items); ``rho2_next`` None
+        marks the last iteration, whose x (times alpha for Poisson) goes to ``out``."""
+        if self.layout is None:
+            raise _lib.EngineError("ADMMState.step before init")
+        if z.dtype != torch.float32 or not z.is_contiguous():
+            z = z.float().contiguous()
         if z.shape != self.y.shape:
             raise ValueError(f"denoiser returned {tuple(z.shape)}, expected {tuple(self.y.shape)}")
-        if self.lib.gd_admm_state_layout(self.H, self.W, self.llh) != self.layout:
+        if z.device != self.dev:
+            raise ValueError(f"denoiser returned a tensor on {z.device}, the state is on {self.dev}")
+        last = rho2_next is None
+        if last:
+            if out is None or out.shape != self.y.shape or out.dtype != torch.float32 or out.device != self.dev \
+                    or not out.is_contiguous():
+                raise ValueError("the last iteration needs a contiguous fp32 `out` shaped like y on the state's device")
+            dst = out
+        else:
+            dst = self.zin
+        if self.llh != 0 and self.lib.gd_admm_state_layout(self.H, self.W, self.llh) != self.layout:
             raise _lib.EngineError("the ADMM state layout changed since init (gd_set_fused_iteration toggled "
                                    "between gd_admm_init and gd_admm_iter)")
-        last = rho2_next is None
-        dst = out if last else self.zin
-        r1, r1s = rho1
-        r2, r2s = rho2
-        rn, rns = (rho2_next if rho2_next is not None else (None, 0))
-        _require_device(z, dst, r1, r2, rn, self.y)
-        with _on(self.dev):
-            ws = workspace(self.N, self.H, self.W, self.dev)
-            _lib.check(self.lib.gd_admm_iter(
-                self.y.data_ptr(), z.data_ptr(), dst.data_ptr(), self.alpha.data_ptr(), self.alpha_s,
-                r1.data_ptr(), r1s, r2.data_ptr(), r2s, None if rn is None else rn.data_ptr(), rns, self.llh,
-                self.iter, int(last), self.N, self.H, self.W, self.state.data_ptr(), ws.data_ptr(),
-                _stream(self.dev)), "gd_admm_iter")
+        r1, r1s = _scalar_arg(rho1, self.dev)
+        r2, r2s = _scalar_arg(rho2, self.dev)
+        rn, rns = (None, 0) if last else _scalar_arg(rho2_next, self.dev)
+        yp, ap, as_, sp, wp = self._fixed
+        args = (yp, z.data_ptr(), dst.data_ptr(), ap, as_, r1, r1s, r2, r2s, rn, rns, self.llh, self.iter, int(last),
+                self.N, self.H, self.W, sp, wp)
+        if torch.cuda.current_device() == self._dev_index:
+            rc = self.lib.gd_admm_iter(*args, torch.cuda.current_stream().cuda_stream)
+        else:
+            with _on(self.dev):
+                rc = self.lib.gd_admm_iter(*args, _stream(self.dev))
+        _lib.check(rc, "gd_admm_iter")
         self.iter += 1
         return dst
 
 
 __all__ = ["psf_to_otf_half", "conv_half", "rfft2_half", "irfft2_half", "wiener", "richardson_lucy",
            "tikhonov", "filter_power", "filter_power_taps", "GaussXState", "gx_x_update",
-           "ADMMState", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos", "subnet_rhos_psf",
+           "ADMMState", "RhoSchedule", "workspace", "empty_otf", "supported", "subnet_features", "subnet_rhos", "subnet_rhos_psf",
            "mlp_supported"]

@@ -32,19 +32,6 @@ from . import engine
 from .nets import SubNet, XDenseUNet, ZUpdateResUNet, ZUpdateXDenseUNet
 
 
-def _rho_view(rho_iters, n, N):
-    """(tensor, stride) for iteration n of a [N,1,1,n] SubNet output or an [n] parameter."""
-    if rho_iters.dim() == 4:
-        col = rho_iters[:, 0, 0, n]
-        if col.dtype != torch.float32:
-            col = col.float().contiguous()
-        return col, (col.stride(0) if col.shape[0] == N and N > 1 else 0)
-    t = rho_iters[n:n + 1]
-    if t.dtype != torch.float32:
-        t = t.float().contiguous()
-    return t, 0
-
-
 class Unrolled_ADMM(nn.Module):
     def __init__(self, n_iters=8, llh="Poisson", denoiser="ResUNet", PnP=True, subnet=True):
         super().__init__()
@@ -99,12 +86,13 @@ class Unrolled_ADMM(nn.Module):
                 zero = torch.zeros(1, device=y.device)
                 st.init((zero, 0))
             return st.zin * st.alpha.view(-1, 1, 1, 1) if self.llh == "Poisson" else st.zin
-        st.init(_rho_view(rho2_iters, 0, N))
+        r1 = engine.RhoSchedule(rho1_iters, N, st.dev)   # (pointer, stride) per iteration, computed once
+        r2 = engine.RhoSchedule(rho2_iters, N, st.dev)
+        st.init(r2[0])
         out = torch.empty_like(st.y)
         for it in range(n):
             z = self.Z(st.zin)
-            nxt = _rho_view(rho2_iters, it + 1, N) if it + 1 < n else None
-            st.step(z, _rho_view(rho1_iters, it, N), _rho_view(rho2_iters, it, N), nxt, out=out)
+            st.step(z, r1[it], r2[it], r2[it + 1] if it + 1 < n else None, out=out)
         return out
 
 

@@ -198,35 +198,65 @@ class SubNet(nn.Module):
                                  nn.Linear(64, 64), nn.ReLU(inplace=True),
                                  nn.Linear(64, self.n_out), nn.Softplus())
 
-    def _packed_params(self):
-        """Folded conv+BN weights of the 8 convs in gd_subnet_features order: per layer w then b, w
-        tap-major ``[cin][3][3][cout]`` (include/gdeconv.h)."""
-        key = tuple(dc._fold_key() for dc in self._double_convs())
-        if getattr(self, "_pack", None) is None or self._pack[0] != key:
+    def _pack_modules(self):
+        """(conv/BN pairs, the 3 Linear layers, the 4 _DoubleConvs), looked up once per module tree."""
+        ident = (id(self.conv_layers), id(self.mlp))
+        c = self.__dict__.get("_pmods")
+        if c is None or c[0] != ident:
+            dcs = [down.maxpool_conv[1] for down in self.conv_layers]
+            pairs = []
+            for dc in dcs:
+                c1, b1, _, c2, b2, _ = dc.double_conv
+                pairs += [(c1, b1), (c2, b2)]
+            c = (ident, pairs, [self.mlp[0], self.mlp[2], self.mlp[4]], dcs)
+            self.__dict__["_pmods"] = c
+        return c[1], c[2], c[3]
+
+    def _pack_key(self):
+        """Data pointers and in-place versions of every tensor the engine packs (8 conv + BN, 3 Linear):
+        changes on load_state_dict, .to(), optimizer steps.  ~15 us, against ~300 us for walking
+        parameters() / buffers() of the module tree on every forward."""
+        pairs, lins, _ = self._pack_modules()
+        ts = []
+        for c, b in pairs:
+            p, q, r = c._parameters, b._parameters, b._buffers
+            ts += (p["weight"], p["bias"], q["weight"], q["bias"], r["running_mean"], r["running_var"])
+        for lin in lins:
+            p = lin._parameters
+            ts += (p["weight"], p["bias"])
+        return tuple(map(torch.Tensor.data_ptr, ts)) + tuple([t._version for t in ts])
+
+    def _engine_pack(self):
+        """(conv pack, MLP pack) for the engine kernels, rebuilt only when a packed tensor changed.
+        Conv pack: folded conv+BN weights of the 8 convs in gd_subnet_features order, per layer w then b,
+        w tap-major ``[cin][3][3][cout]`` (include/gdeconv.h).  MLP pack: W1^T | b1 | W2^T | b2 | W3^T |
+        b3 (transposed nn.Linear weights) for gd_subnet_rhos."""
+        key = self._pack_key()
+        c = self.__dict__.get("_epack")
+        if c is None or c[0] != key:
+            pairs, lins, _ = self._pack_modules()
             with torch.no_grad():
                 parts = []
-                for dc in self._double_convs():
-                    c1, b1, _, c2, b2, _ = dc.double_conv
-                    for conv, bn in ((c1, b1), (c2, b2)):
-                        w, b = _fold_conv_bn(conv, bn)
-                        parts += [w.permute(1, 2, 3, 0).reshape(-1), b.reshape(-1)]
-                self._pack = (key, torch.cat(parts).float().contiguous())
-        return self._pack[1]
+                for conv, bn in pairs:
+                    w, b = _fold_conv_bn(conv, bn)
+                    parts += [w.permute(1, 2, 3, 0).reshape(-1), b.reshape(-1)]
+                conv_pack = torch.cat(parts).float().contiguous()
+                parts = []
+                for m in lins:
+                    parts += [m.weight.t().reshape(-1), m.bias.reshape(-1)]
+                mlp_pack = torch.cat(parts).float().contiguous()
+            c = (key, conv_pack, mlp_pack)
+            self.__dict__["_epack"] = c
+        return c[1], c[2]
+
+    def _packed_params(self):
+        return self._engine_pack()[0]
 
     def _packed_mlp(self):
-        """W1^T | b1 | W2^T | b2 | W3^T | b3 of the MLP (transposed nn.Linear weights) for gd_subnet_rhos."""
-        lin = [self.mlp[0], self.mlp[2], self.mlp[4]]
-        key = tuple((m.weight._version, m.bias._version, m.weight.data_ptr()) for m in lin)
-        if getattr(self, "_mpack", None) is None or self._mpack[0] != key:
-            with torch.no_grad():
-                parts = []
-                for m in lin:
-                    parts += [m.weight.t().reshape(-1), m.bias.reshape(-1)]
-                self._mpack = (key, torch.cat(parts).float().contiguous())
-        return self._mpack[1]
+        return self._engine_pack()[1]
 
     def _double_convs(self):
-        return [down.maxpool_conv[1] for down in self.conv_layers]
+        return self._pack_modules()[2]
 
     def _engine_ok(self, kernel):
         h, w = kernel.shape[-2:]
@@ -249,18 +279,20 @@ class SubNet(nn.Module):
             # MLP stays in PyTorch after k_subnet_features so its parameters get gradients)
             from . import engine
             dev = kernel.device
+            cpack, mpack = self._engine_pack()
+            if cpack.device != dev:
+                cpack, mpack = cpack.to(dev), mpack.to(dev)
             mlp_ok = engine.mlp_supported(self.n_out)  # k_subnet_mlp: n_out <= 64 (kMaxOut)
             if mlp_ok and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
                 if h <= 64:  # |FFT2(pad128(psf))|^2 inside the feature kernel (no OTF128 pre-pass)
-                    out = engine.subnet_rhos_psf(kernel, self._packed_params().to(dev), self._packed_mlp().to(dev),
-                                                 alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                    out = engine.subnet_rhos_psf(kernel, cpack, mpack, alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
                 else:
-                    out = engine.subnet_rhos(engine.psf_to_otf_half(kernel, N, 128, 128), self._packed_params().to(dev),
-                                             self._packed_mlp().to(dev), alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                    out = engine.subnet_rhos(engine.psf_to_otf_half(kernel, N, 128, 128), cpack, mpack,
+                                             alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
                 if self.n_out == self.n:
                     return out.view(N, 1, 1, self.n)
                 return out[:, :, 0:self.n].view(N, 1, 1, self.n), out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
-            feat = engine.subnet_features(engine.psf_to_otf_half(kernel, N, 128, 128), self._packed_params().to(dev))
+            feat = engine.subnet_features(engine.psf_to_otf_half(kernel, N, 128, 128), cpack)
         else:
             h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2
             w1, w2 = (128 - w) // 2, 128 - w - (128 - w) // 2

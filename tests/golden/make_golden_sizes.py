@@ -39,8 +39,10 @@ from models.Wiener import Wiener               # noqa: E402  (reference)
 from utils.utils_torch import conv_fft_batch, psf_to_otf  # noqa: E402  (reference)
 
 WEIGHT_SEED = 1234
-# (H, W, psf side): a radix-2/5 square, a non-square pair, an odd side, a prime side, radix 3 and 5
-SIZES = [(40, 40, 32), (64, 48, 32), (45, 60, 32), (97, 80, 48), (192, 160, 48)]
+# (H, W, psf side): a radix-2/5 square, a non-square pair, an odd side, a prime side, radix 3 and 5,
+# odd widths
+SIZES = [(40, 40, 32), (64, 48, 32), (45, 60, 32), (97, 80, 48), (192, 160, 48),
+         (45, 61, 32), (255, 255, 48)]  # odd W (no Nyquist column): 61 prime, 255 = 3 5 17
 LAM = 0.37
 
 

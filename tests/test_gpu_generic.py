@@ -12,7 +12,7 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160)]   # sizes.npz
+SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160), (45, 61), (255, 255)]   # sizes.npz (odd W last)
 FFT_SIZES = [(2, 2), (3, 5), (17, 19), (40, 40), (64, 48), (45, 60), (97, 80), (243, 125), (1000, 30),
              (7, 1024), (1024, 1024), (96, 256), (256, 255)]
 

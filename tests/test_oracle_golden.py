@@ -221,7 +221,7 @@ def test_gauss2x_gradients():
 
 
 # ------------------------------------------------------------------ sizes outside the compile-time set
-SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160)]  # tests/golden/make_golden_sizes.py
+SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160), (45, 61), (255, 255)]  # tests/golden/make_golden_sizes.py
 
 
 @pytest.mark.parametrize("H,W", SIZES)
@@ -258,3 +258,34 @@ def test_generic_size_full_model_and_gauss2x():
     assert torch.equal(out, T(g["full_out"]))
     out = O.gx_forward(T(g["gx_obs"]), T(g["gx_psf"]), T(g["gx_alpha"]), T(g["gx_rho"]))
     assert torch.equal(out, T(g["gx_out"]))
+
+
+def test_pixel_max_is_noise_between_two_reference_fft_paths():
+    """Why tests/test_gpu_pixel_parity.py bounds the tail (p99, 32nd-largest pixel), not the max, of the floored
+    per-pixel error: two equally valid fp32 FFT paths of the reference itself - torch.fft.fftn (the
+    reference's) and torch.fft.rfft2 - measured against fp64 on the golden inputs.  The max ratio
+    scatters beyond 2x (it is one near-zero pixel's rounding draw), the tail ratios do not."""
+    def wiener_rfft(y, psf, alpha):
+        _, H = O.psf_to_otf(psf, y.size(), dtype=y.dtype)
+        Hh = H[..., : y.shape[-1] // 2 + 1]
+        return torch.fft.irfft2(torch.conj(Hh) * torch.fft.rfft2(y) / (torch.abs(Hh) ** 2 + 350 / alpha),
+                                s=y.shape[-2:])
+
+    def quant(a, ref):  # p99 and the 32nd-largest pixel (tests/test_gpu_pixel_parity.py:pix_quantiles)
+        a, ref = a.double().reshape(a.shape[0], -1), ref.double().reshape(ref.shape[0], -1)
+        den = torch.maximum(ref.abs(), 1e-5 * ref.abs().amax(1, keepdim=True))
+        r = ((a - ref).abs() / den).flatten()
+        return [float(torch.quantile(r, 0.99)), float(torch.topk(r, 32).values[-1])]
+
+    g = golden("sizes.npz")
+    max_ratios = []
+    for s in ("40x40", "64x48", "45x60", "97x80", "192x160", "45x61", "255x255"):
+        o, p, a = (T(g[f"{s}_{k}"]) for k in ("obs", "psf", "alpha"))
+        ref64 = O.wiener(o.double(), p.double(), a.double())
+        gold, alt = T(g[f"{s}_wiener"]), wiener_rfft(o, p, a)
+        assert float(O.normwise_error(gold, ref64).max()) < 1e-6 and float(O.normwise_error(alt, ref64).max()) < 1e-6
+        max_ratios.append(float(O.pixel_error_floored(alt, ref64).max()) / float(O.pixel_error_floored(gold, ref64).max()))
+        qa, qg = quant(alt, ref64), quant(gold, ref64)
+        assert all(x <= 2.0 * y for x, y in zip(qa, qg)), (s, qa, qg)
+    print("max ratios rfft2/fftn:", [round(r, 2) for r in max_ratios])
+    assert max(max_ratios) > 2.0 and min(max_ratios) < 0.5
