@@ -525,7 +525,7 @@ def main():
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
     if args.traffic_json is None:
-        suffix = "_rl" if rl else ("" if L == 256 else f"_{L}")
+        suffix = "_rl" if rl else ("_poisson" if args.llh == "Poisson" else "") + ("" if L == 256 else f"_{L}")
         args.traffic_json = os.path.join(ROOT, "profiles", f"pmc_traffic{suffix}.json")
     try:
         with open(args.traffic_json) as f:

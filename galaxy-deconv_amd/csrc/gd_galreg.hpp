@@ -129,6 +129,9 @@ __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float
 #ifndef GD_REG_DEPTH
 #define GD_REG_DEPTH 2
 #endif
+#ifndef GD_POIS_DEPTH
+#define GD_POIS_DEPTH 2  // Poisson pass A
+#endif
 
 struct SGroup {
     f4v h, g[2], u[2], w[2];
@@ -289,7 +292,8 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         const float* z = a.a0 + (size_t)g * L * L;
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
+            // opaque: no 64-bit row offset CSE'd with phase I's stores and kept live in between
+            const float* r0 = z + (size_t)(2 * (opaque(line) + LINES * q)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
         }
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
         nyqc[tid] = gauss_bin4<L, POIS>(a, g, tid, nyqc[tid], r1, r2, r2n, first, last);
     }
-    fused_update4x<L, RG::CPL, POIS>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
+    fused_update4x<L, RG::CPL, POIS, POIS ? GD_POIS_DEPTH : GD_REG_DEPTH>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
     lds_barrier();  // Nyquist results
     GD_TRACE(4);
 #pragma unroll
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CA[u], opaque(j), my, tw);
-        if (GD_REG_PINI) pin(CA[u]);
+        if (GD_REG_PINI || POIS) pin(CA[u]);  // Poisson pass A: spill-free with the inverses pinned
         __builtin_amdgcn_sched_barrier(0);
     }
     if (l0) {
@@ -417,11 +421,12 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         if (GD_REG_PINF) pin(CB[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
-    fused_update4x<L, RG::CPL, POIS>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last);
+    fused_update4x<L, RG::CPL, POIS, POIS ? GD_POIS_DEPTH : GD_REG_DEPTH>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first,
+                                                                      last);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CB[u], opaque(j), my, tw);
-        if (GD_REG_PINI) pin(CB[u]);
+        if (GD_REG_PINI || POIS) pin(CB[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -471,7 +476,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
             reg_fft<L, true>(V[w], opaque(j), my, tw);
-            float* o = out + (size_t)(hf * L / 2 + 2 * (line + LINES * w)) * L + j;
+            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
             if constexpr (POIS) {
                 if (last) {  // x * alpha for Poisson (:215)
 #pragma unroll
@@ -514,6 +519,12 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
     kx = opaque(kx);
     __builtin_amdgcn_sched_barrier(0);
     const size_t gb = (size_t)g * (L / 2 + 1) * L;
+    if constexpr (POIS) {  // Poisson two-pass: the OTF itself in the G slot (pass B needs H), stored first
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            *reinterpret_cast<f4v*>(a.s_g + gb + soff_c(kx, m, j)) =
+                f4v{Hc[2 * m].x, Hc[2 * m].y, Hc[2 * m + 1].x, Hc[2 * m + 1].y};
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         f4v h4, g4[2];
@@ -524,14 +535,16 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
             const float hh = Hk.x * Hk.x + Hk.y * Hk.y;  // init_bin's arithmetic
             const float2 Gk = cmulc(C[s], Hk);
             h4[e] = hh;
-            g4[h][c] = POIS ? Hk.x : Gk.x;  // Poisson two-pass: the OTF in the G slot (pass B needs H)
-            g4[h][c + 1] = POIS ? Hk.y : Gk.y;
+            g4[h][c] = Gk.x;
+            g4[h][c + 1] = Gk.y;
             const float rl = __builtin_amdgcn_rcpf(hh + ial);  // lhs = HtH + 1/alpha; one reciprocal (1 ulp), not two divisions
             C[s] = cscale(make_float2(Gk.x * rl, Gk.y * rl), inv_n);
         }
         *reinterpret_cast<f4v*>(a.s_hh + gb + soff_h(kx, q, j)) = h4;
+        if constexpr (!POIS) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) *reinterpret_cast<f4v*>(a.s_g + gb + soff_c(kx, 2 * q + h, j)) = g4[h];
+            for (int h = 0; h < 2; ++h) *reinterpret_cast<f4v*>(a.s_g + gb + soff_c(kx, 2 * q + h, j)) = g4[h];
+        }
     }
 }
 // One column of F(x0) (C) into the W~ slot: iteration 0 forms W~1 from it (defer_w1 at 256^2)
@@ -591,7 +604,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     float2* my = S + line * RG::XCH;
     float2* park = S + RG::XA;
     fill_twiddles<L>(tw, tid, T);
-    const float al = a.alpha(g), r2n = a.rho2n(g);
+    const float al = a.alpha(g), r2n = POIS ? 0.f : a.rho2n(g);  // Poisson: pass B<INIT> takes the V step
     GD_TRACE(0);
 
     // R: max(y, 0) / alpha (RF_YA), as a multiply by the galaxy's 1/alpha (within an ulp of the division;
@@ -602,7 +615,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         const float* y = a.y + (size_t)g * L * L;
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q) {
-            const float* r0 = y + (size_t)(2 * (line + LINES * q)) * L + j;
+            const float* r0 = y + (size_t)(2 * (opaque(line) + LINES * q)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) * ial, fmaxf(r0[L + F1 * r], 0.f) * ial);
         }
@@ -657,6 +670,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false>(CA[u], opaque(j), my, tw);
+            if (POIS) pin(CA[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
         if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
@@ -692,6 +706,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 reg_fft<L, true>(CA[u], opaque(j), my, tw);
+                if (POIS) pin(CA[u]);  // the Poisson init: materialised here, spill-free
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (l0) {
@@ -747,6 +762,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
                 init_update4<L, POIS>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
+                if (POIS) pin(CB[u]);
             } else {
                 w1_update4<L>(a, CB[u], g, KS + line + LINES * u, j);
             }
@@ -804,7 +820,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         for (int w = 0; w < RG::HPL; ++w) {
             float2 (&V)[F2] = X[2 * hf + w];
             reg_fft<L, true>(V, opaque(j), my, tw);
-            float* o = out + (size_t)(hf * L / 2 + 2 * (line + LINES * w)) * L + j;
+            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
                 V[r] = make_float2(fminf(fmaxf(V[r].x, 0.f), 1.f), fminf(fmaxf(V[r].y, 0.f), 1.f));

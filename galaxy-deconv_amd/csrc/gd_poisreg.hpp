@@ -87,6 +87,7 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
                 col_load(ld, (i + 1 < RG::CPL ? 0 : KS) + line + LINES * ((i + 1) % RG::CPL));
             __builtin_amdgcn_sched_barrier(0);
             reg_fft<L, true>(C, opaque(j), my, tw);
+            pin(C);  // materialised here: spill-free (2 VGPRs spilled across phase I otherwise)
             __builtin_amdgcn_sched_barrier(0);
         });
     }

@@ -177,6 +177,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 reg_fft<L, true>(CA[u], opaque(j), my, tw);
+                pin(CA[u]);  // the column results materialised here (spill-free register allocation)
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (l0) {
@@ -214,6 +215,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                 reg_fft<L, false>(CB[u], opaque(j), my, tw);
                 hmul(CB[u], KS + line + LINES * u);
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
+                pin(CB[u]);
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll

@@ -24,8 +24,18 @@ import torch
 from . import _lib
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)   # hipStream_t of (device index)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream(device=None):
+    if _raw_stream is not None and device is not None and device.index is not None:
+        return _raw_stream(device.index)
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def _current_device():
+    return _cur_device() if _cur_device is not None else torch.cuda.current_device()
 
 
 def _require_device(*ts):
@@ -47,7 +57,7 @@ def _require_device(*ts):
 def _on(device):
     """Make ``device`` current for the duration of one engine call (the C side picks its internal
     pipeline streams by the current HIP device); no device switch when it already is."""
-    if device.index is None or torch.cuda.current_device() == device.index:
+    if device.index is None or _current_device() == device.index:
         yield
         return
     with torch.cuda.device(device):
@@ -604,8 +614,8 @@ class ADMMState:
         yp, ap, as_, sp, wp = self._fixed
         args = (yp, z.data_ptr(), dst.data_ptr(), ap, as_, r1, r1s, r2, r2s, rn, rns, self.llh, self.iter, int(last),
                 self.N, self.H, self.W, sp, wp)
-        if torch.cuda.current_device() == self._dev_index:
-            rc = self.lib.gd_admm_iter(*args, torch.cuda.current_stream().cuda_stream)
+        if _current_device() == self._dev_index:
+            rc = self.lib.gd_admm_iter(*args, _stream(self.dev))
         else:
             with _on(self.dev):
                 rc = self.lib.gd_admm_iter(*args, _stream(self.dev))

@@ -140,6 +140,14 @@ def main():
         out["kernels"][f"op_admm_iter<{L},Poisson>"] = {
             "hbm_bytes_per_launch": (ptot - init_b * out["kernels"][f"k_pois_b<{L}>"]["hbm_bytes_per_launch"]) / a.iters,
             "launches": a.iters, "note": "Poisson two-pass: pass A + pass B per call (the init's pass B excluded)"}
+    if f"k_gal_init<{L},POIS>" in out["kernels"] and f"k_pois_b<{L}>" in out["kernels"]:
+        pi = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},POIS>"]
+        out["kernels"][f"op_admm_init<{L},Poisson>"] = {
+            "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in pi if k in out["kernels"])
+            + out["kernels"][f"k_pois_b<{L}>"]["hbm_bytes_per_launch"],
+            "launches": out["kernels"][f"k_gal_init<{L},POIS>"]["launches"],
+            "note": "Poisson init: k_psf_rows<STATE> + k_gal_reg_init<POIS> + one pass B (its per-launch average "
+                    "over the init's and the iterations' launches)"}
     init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
     if f"k_gal_init<{L},ONE>" in out["kernels"]:
         init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},ONE>"]
