@@ -119,12 +119,11 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:
-            # two-pass (gd_poisreg.hpp): pass A z, |H|^2, U1, W~ in, U1, X, zin out (2 img + 4.5 half; first
-            # 3.5: no U1; last 2 img + 2.5 half: nothing but x written); pass B X, H, w, y in, w, W~ out
-            # (3 img + 3 half)
+            # two-pass (gd_poisreg.hpp): pass A z, H, U1, W in, U1, H X, zin out (2 img + 5 half; first 4: no
+            # U1; last 2 img + 3 half: nothing but x written); pass B H X, y, w in, w, F(w') out (3 img + 2 half)
             if n == 1:
-                return 2 * img + 1.5 * half
-            mid, first, last = 5 * img + 7.5 * half, 5 * img + 6.5 * half, 2 * img + 2.5 * half
+                return 2 * img + 2 * half
+            mid, first, last = 5 * img + 7 * half, 5 * img + 6 * half, 2 * img + 3 * half
             return (first + mid * (n - 2) + last) / n
         # u1, w (= v - u2), z in; u1, w, zin out (+ y, the OTF half spectrum); the last iteration
         # reads z, u1, w, y, OTF and writes x only

@@ -693,7 +693,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
             // iteration 0's W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2): the V step
             // (models/Unrolled_ADMM.py:335-336) with Hx = H X0 and u2 = 0, premultiplied by conj(H)
             if constexpr (defer_w1<L>()) {
-                if (valid) a.s_w[sflat_c<L>(ob + ky)] = P[s];  // F(x0): the first iteration forms W~1
+                // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
+                if (valid)
+                    a.s_w[sflat_c<L>(ob + ky)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(ob + ky)], P[s]) : P[s];
             } else {
                 const float hh = a.s_hh[sflat_h<L>(ob + ky)];
                 const float2 Gk = a.s_g[sflat_c<L>(ob + ky)];
@@ -985,7 +987,8 @@ __device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, f
 template <int L>
 __device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk, float r2n) {
     if constexpr (defer_w1<L>()) {
-        a.s_w[sflat_c<L>(o)] = Xk;  // F(x0): the first iteration forms W~1
+        // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
+        a.s_w[sflat_c<L>(o)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(o)], Xk) : Xk;
     } else {
         const float hh = a.s_hh[sflat_h<L>(o)];
         const float2 Gk = a.s_g[sflat_c<L>(o)];
@@ -2373,7 +2376,7 @@ struct Ops {
             }));
         }
         Args b = a0;
-        b.s_x = a0.s_w;  // X := F(x0)
+        b.s_x = a0.s_w;  // H X := H F(x0), left in the W slot by the init
         return Lc::pois_b(b, 1, st0);
     }
     static int admm_iter_pois2(Args a, hipStream_t st0) {
@@ -2574,7 +2577,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r03.1"; }
+const char* gd_engine_rev(void) { return "r03.2"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2644,7 +2647,7 @@ size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
     if (llh == GD_LLH_GAUSSIAN) return (spec / 8 + 1) / 2 * 8 + 3 * spec;  // |H|^2 padded to 8-byte alignment
     // Poisson: [otf | u1 | w] (three-kernel chain); at 256^2 also room for the two-pass layout
-    // [|H|^2 | H | U1 | W~ | X] + w (bind_state picks the layout from gd_set_fused_iteration)
+    // [(|H|^2) | H | U1 | F(w) | H X] + w (bind_state picks the layout from gd_set_fused_iteration)
     return (H == 256 && W == 256) ? std::max(spec + 2 * img, spec / 2 + 4 * spec + img) : spec + 2 * img;
 }
 
@@ -2660,8 +2663,8 @@ void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
         float2* c = base + spec / 2;
         a.s_g = c;                 // the OTF H
         a.s_u1 = c + spec;
-        a.s_w = c + 2 * spec;      // conj(H) F(w)
-        a.s_x = c + 3 * spec;      // X (pass A -> pass B)
+        a.s_w = c + 2 * spec;      // F(w), w = v - u2 (pass B -> pass A, which multiplies by conj(H))
+        a.s_x = c + 3 * spec;      // H X (pass A -> pass B)
         a.o1 = reinterpret_cast<float*>(c + 4 * spec);  // w = v - u2 (spatial)
         return;
     }

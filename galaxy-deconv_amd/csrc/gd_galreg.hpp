@@ -76,17 +76,21 @@ __device__ __forceinline__ void st4v(void* p, f4v v) {
 #endif
 }
 
-// Poisson pass A's bin (the X update and u1's dual, models/Unrolled_ADMM.py:209, :212, on spectra): W~
-// holds conj(H) F(w) with w = v - u2 (written by pass B), so X = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2
-// + rho2), U1' = (U1 + X) - Z; returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last); Xo = X
-// (pass B's input)
-__device__ __forceinline__ float2 pois_math(float hh, float2 U1, float2 Wt, float2 Zk, float r1, float r2, float inv_n,
-                                            float2& U1o, float2& Xo, bool last) {
+// Poisson pass A's bin (the X update and u1's dual, models/Unrolled_ADMM.py:209, :212, on spectra).  The
+// state holds H (the OTF, G slot) and W = F(w), w = v - u2 (written by pass B, unmultiplied), so pass A
+// forms W~ = conj(H) W and |H|^2 (the init's arithmetic) itself: X = (rho1 (Z - U1) + rho2 W~) / (rho1
+// |H|^2 + rho2), U1' = (U1 + X) - Z; returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last);
+// HXo = H X, pass B's only spectral input (pass B reads neither H nor X: one half spectrum less per
+// iteration, and no second read of H for its W~)
+__device__ __forceinline__ float2 pois_math(float2 Hk, float2 U1, float2 Wf, float2 Zk, float r1, float r2, float inv_n,
+                                            float2& U1o, float2& HXo, bool last) {
+    const float hh = Hk.x * Hk.x + Hk.y * Hk.y;
+    const float2 Wt = cmulc(Wf, Hk);
     const float lhs = r1 * hh + r2;
     const float2 A = csub(Zk, U1);
     const float rl = __builtin_amdgcn_rcpf(lhs);
     const float2 X = make_float2((r1 * A.x + r2 * Wt.x) * rl, (r1 * A.y + r2 * Wt.y) * rl);
-    Xo = X;
+    HXo = cmul(Hk, X);
     if (last) return cscale(X, inv_n);
     const float2 U1n = csub(cadd(U1, X), Zk);
     U1o = U1n;
@@ -100,17 +104,17 @@ __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float
     constexpr float inv_n = float(1.0 / double(L * L));
     const size_t cb = ((size_t)g * (L / 2 + 1) + L / 2) * L;
     const int pc = sidx_c<L>(ky);
-    const float hh = a.s_hh[cb + sidx_h<L>(ky)];
     if constexpr (POIS) {
         const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
-        float2 U1n, Xo;
-        const float2 r = pois_math(hh, U1, a.s_w[cb + pc], Zk, r1, r2, inv_n, U1n, Xo, last);
+        float2 U1n, HXo;
+        const float2 r = pois_math(a.s_g[cb + pc], U1, a.s_w[cb + pc], Zk, r1, r2, inv_n, U1n, HXo, last);
         if (!last) {
             st_s(a.s_u1 + cb + pc, U1n);
-            st_s(a.s_x + cb + pc, Xo);
+            st_s(a.s_x + cb + pc, HXo);
         }
         return r;
     }
+    const float hh = a.s_hh[cb + sidx_h<L>(ky)];
     const float2 Gk = (last && !first) ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
     const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
     float2 Wt = a.s_w[cb + pc];
@@ -139,11 +143,12 @@ struct SGroup {
 template <int L, bool POIS = false>
 __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb, int kx, int q, int j, bool first,
                                             bool last) {
-    G.h = ld4v(a.s_hh + gb + soff_h(kx, q, j));
+    G.h = POIS ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_hh + gb + soff_h(kx, q, j));  // Poisson: |H|^2 from H
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const size_t off = gb + soff_c(kx, 2 * q + h, j);
-        G.g[h] = (POIS || (last && !first)) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);  // first: W~1 needs G
+        // Gaussian G (first: W~1 needs it; not on the last); Poisson: the OTF H (the G slot)
+        G.g[h] = (!POIS && last && !first) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);
         G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_u1 + off);
         G.w[h] = ld4v(a.s_w + off);
     }
@@ -171,8 +176,8 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
             float2 U1n, Wn;
             const float2 Gk = make_float2(G[t].g[h][c], G[t].g[h][c + 1]);
             float2 Wt = make_float2(G[t].w[h][c], G[t].w[h][c + 1]);
-            if constexpr (POIS) {  // Wn carries X (pass B's input)
-                C[u][4 * q + e] = pois_math(G[t].h[e], make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt, C[u][4 * q + e],
+            if constexpr (POIS) {  // Gk carries H, Wt the unmultiplied F(w), Wn H X (pass B's input)
+                C[u][4 * q + e] = pois_math(Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt, C[u][4 * q + e],
                                             r1, r2, inv_n, U1n, Wn, last);
             } else {
                 if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
@@ -540,15 +545,17 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
             const float rl = __builtin_amdgcn_rcpf(hh + ial);  // lhs = HtH + 1/alpha; one reciprocal (1 ulp), not two divisions
             C[s] = cscale(make_float2(Gk.x * rl, Gk.y * rl), inv_n);
         }
-        *reinterpret_cast<f4v*>(a.s_hh + gb + soff_h(kx, q, j)) = h4;
-        if constexpr (!POIS) {
+        if constexpr (!POIS) {  // (Poisson: pass A derives |H|^2 from H)
+            *reinterpret_cast<f4v*>(a.s_hh + gb + soff_h(kx, q, j)) = h4;
 #pragma unroll
             for (int h = 0; h < 2; ++h) *reinterpret_cast<f4v*>(a.s_g + gb + soff_c(kx, 2 * q + h, j)) = g4[h];
         }
     }
 }
 // One column of F(x0) (C) into the W~ slot: iteration 0 forms W~1 from it (defer_w1 at 256^2)
-template <int L>
+// POIS: H F(x0) instead (pass B<INIT>'s input, as pass A leaves H X for pass B); H is the G slot this
+// thread wrote for the same column in the init's column pass
+template <int L, bool POIS = false>
 __device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16], int g, int kx, int j) {
     static_assert(defer_w1<L>(), "the fused init defers W~1 to the first iteration");
     j = opaque(j);
@@ -556,8 +563,15 @@ __device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16],
     __builtin_amdgcn_sched_barrier(0);
     const size_t gb = (size_t)g * (L / 2 + 1) * L;
 #pragma unroll
-    for (int m = 0; m < 8; ++m)
-        st4v(a.s_w + gb + soff_c(kx, m, j), f4v{C[2 * m].x, C[2 * m].y, C[2 * m + 1].x, C[2 * m + 1].y});
+    for (int m = 0; m < 8; ++m) {
+        float2 c0 = C[2 * m], c1 = C[2 * m + 1];
+        if constexpr (POIS) {
+            const f4v h = ld4v(a.s_g + gb + soff_c(kx, m, j));
+            c0 = cmul(make_float2(h[0], h[1]), c0);
+            c1 = cmul(make_float2(h[2], h[3]), c1);
+        }
+        st4v(a.s_w + gb + soff_c(kx, m, j), f4v{c0.x, c0.y, c1.x, c1.y});
+    }
 }
 // The OTF column kx (FFT'd, LDS exchange) from the PSF's compact row spectra; line 0 (kx = 0, packed
 // with the real Nyquist column) splits it and leaves the Nyquist column's spectrum in nyqh.
@@ -718,7 +732,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
                 w1_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], r2n);
 #pragma unroll
-            for (int u = 0; u < RG::CPL; ++u) w1_update4<L>(a, CA[u], g, line + LINES * u, j);
+            for (int u = 0; u < RG::CPL; ++u) w1_update4<L, POIS>(a, CA[u], g, line + LINES * u, j);
         }
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q)
@@ -764,7 +778,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
                 if (POIS) pin(CB[u]);
             } else {
-                w1_update4<L>(a, CB[u], g, KS + line + LINES * u, j);
+                w1_update4<L, POIS>(a, CB[u], g, KS + line + LINES * u, j);
             }
             __builtin_amdgcn_sched_barrier(0);
         }

@@ -2,16 +2,18 @@
 // V_Update_Poisson :326-328).  The Poisson V step (sqrt) keeps v, hence w = v - u2, in the image domain,
 // so an iteration needs the spectra of two images and two inverse transforms: more than one CU holds
 // at once.  Split where the data are smallest:
-//   pass A  k_gal_reg<L, true> (gd_galreg.hpp): z -> Z;  X = (rho1 (Z - U1) + rho2 W~) / (rho1 |H|^2 + rho2);
-//           U1' = (U1 + X) - Z;  zin = F^-1(X + U1')  (last: x alpha);  X -> the X slot
-//   pass B  k_pois_b<L> (here): HX = H X -> Hx (column then row inverses);  u2 = Hx - w;
-//           v' = V(Hx + u2, y, rho2', alpha);  w' = v' - u2 -> out;  W~' = conj(H) F(w') -> state
-// with U1 = F(u1) and W~ = conj(H) F(w) kept as spectra (the linear steps :209, :212 on spectra, as the
-// Gaussian engine does).  Compulsory bytes per galaxy and iteration: pass A 2 img + 4.5 half, pass B
-// 3 img + 3 half (+ the OTF re-read by its W~ columns), against 10 img + 7 half through the workspace
-// for the three-kernel chain.  State at 256^2: [|H|^2 | H (the G slot) | U1 | W~ | X] + w (image).
-// The init (INIT = 1): k_gal_reg_init<L, true> leaves F(x0) in the W~ slot and the OTF in the G slot;
-// pass B with X := F(x0) and u2 = 0 forms w1 = v1 = V(H x0) and W~1 (RI_INIT's arithmetic).
+//   pass A  k_gal_reg<L, true> (gd_galreg.hpp): z -> Z;  W~ = conj(H) W;  X = (rho1 (Z - U1) + rho2 W~) /
+//           (rho1 |H|^2 + rho2);  U1' = (U1 + X) - Z;  zin = F^-1(X + U1')  (last: x alpha);  H X -> the X slot
+//   pass B  k_pois_b<L> (here): H X -> Hx (column then row inverses);  u2 = Hx - w;
+//           v' = V(Hx + u2, y, rho2', alpha);  w' = v' - u2 -> out;  W' = F(w') -> state
+// with U1 = F(u1) and W = F(w) kept as spectra (the linear steps :209, :212 on spectra, as the Gaussian
+// engine does).  H (the OTF) is read once per iteration, by pass A, which multiplies W by conj(H) and X by
+// H: pass B's only spectral input is H X and its only spectral output F(w').  Compulsory bytes per galaxy
+// and iteration: pass A 2 img + 5 half, pass B 3 img + 2 half, against 10 img + 7 half through the
+// workspace for the three-kernel chain (and 5 img + 8.5 half when pass B read H and X, and H twice).
+// State at 256^2: [(|H|^2, unused) | H (the G slot) | U1 | W | H X] + w (image).
+// The init (INIT = 1): k_gal_reg_init<L, true> leaves the OTF in the G slot and H F(x0) in the W slot;
+// pass B with H X := H F(x0) and u2 = 0 forms w1 = v1 = V(H x0) and W1 = F(w1) (RI_INIT's arithmetic).
 // Included inside namespace gd by gd_engine.hip (after gd_galreg.hpp).
 
 #ifndef GD_POIS_PC
@@ -37,31 +39,26 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
     const float al = a.alpha(g), r2n = a.rho2n(g);
     const bool init = __builtin_amdgcn_readfirstlane(init_flag) != 0;
     const size_t gb = (size_t)g * K * L;
-    const float* H = reinterpret_cast<const float*>(a.s_g);
-    const float* Xs = reinterpret_cast<const float*>(a.s_x);
+    const float* HXs = reinterpret_cast<const float*>(a.s_x);
     __syncthreads();  // twiddles
     GD_TRACE(0);
 
-    // C1: column kx of H X / L^2 (16-byte loads of both spectra in the lines' register order); the next
+    // C1: column kx of H X / L^2 (pass A's product; 16-byte loads in the lines' register order); the next
     // column's loads are issued before this column's inverse FFT
     struct ColLd {
-        f4v x[F2 / 2], h[F2 / 2];
+        f4v x[F2 / 2];
     };
     auto col_load = [&](ColLd& c, int kx) {
         kx = opaque(kx);
         const int jj = opaque(j);
 #pragma unroll
-        for (int m = 0; m < F2 / 2; ++m) {
-            const size_t off = 2 * (gb + soff_c(kx, m, jj));
-            c.x[m] = ld4v(Xs + off);
-            c.h[m] = ld4v(H + off);
-        }
+        for (int m = 0; m < F2 / 2; ++m) c.x[m] = ld4v(HXs + 2 * (gb + soff_c(kx, m, jj)));
     };
     auto col_hx = [&](float2 (&C)[F2], const ColLd& c) {
 #pragma unroll
         for (int m = 0; m < F2 / 2; ++m) {
-            C[2 * m] = cscale(cmul(make_float2(c.h[m][0], c.h[m][1]), make_float2(c.x[m][0], c.x[m][1])), inv_n);
-            C[2 * m + 1] = cscale(cmul(make_float2(c.h[m][2], c.h[m][3]), make_float2(c.x[m][2], c.x[m][3])), inv_n);
+            C[2 * m] = cscale(make_float2(c.x[m][0], c.x[m][1]), inv_n);
+            C[2 * m + 1] = cscale(make_float2(c.x[m][2], c.x[m][3]), inv_n);
         }
     };
     float2 CA[RG::CPL][F2], CB[RG::CPL][F2];
@@ -184,24 +181,14 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
         GD_TRACE(2 + hf);
     });
 
-    // W: F(w')'s columns, times conj(H) -> W~' (unnormalised, as F(z) in pass A)
-    auto h_load = [&](f4v (&hv)[F2 / 2], int kx) {
-        kx = opaque(kx);
-        const int jj = opaque(j);
-#pragma unroll
-        for (int m = 0; m < F2 / 2; ++m) hv[m] = ld4v(H + 2 * (gb + soff_c(kx, m, jj)));
-    };
-    auto wt_store = [&](const float2 (&C)[F2], const f4v (&hv)[F2 / 2], int kx) {
+    // W: F(w')'s columns -> the W slot (unnormalised, as F(z) in pass A, which multiplies by conj(H))
+    auto wt_store = [&](const float2 (&C)[F2], int kx) {
         kx = opaque(kx);
         const int jj = opaque(j);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int m = 0; m < F2 / 2; ++m) {
-            const size_t off = gb + soff_c(kx, m, jj);
-            const float2 w0 = cmulc(C[2 * m], make_float2(hv[m][0], hv[m][1]));
-            const float2 w1 = cmulc(C[2 * m + 1], make_float2(hv[m][2], hv[m][3]));
-            st4v(a.s_w + off, f4v{w0.x, w0.y, w1.x, w1.y});
-        }
+        for (int m = 0; m < F2 / 2; ++m)
+            st4v(a.s_w + gb + soff_c(kx, m, jj), f4v{C[2 * m].x, C[2 * m].y, C[2 * m + 1].x, C[2 * m + 1].y});
     };
     lds_barrier();  // exchange areas -> slice A
 #pragma unroll
@@ -232,9 +219,6 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
     for (int q = 0; q < RG::PPL; ++q)
 #pragma unroll
         for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
-    f4v hvA[RG::CPL][F2 / 2];  // slice A's OTF columns, loaded under the column FFTs
-#pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) h_load(hvA[u], line + LINES * u);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
@@ -255,12 +239,9 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
         wave_lds_sync();
     }
     lds_barrier();  // nyqc complete
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
-        const size_t o = ((size_t)g * K + L / 2) * L + sidx_c<L>(tid);
-        a.s_w[o] = cmulc(nyqc[tid], a.s_g[o]);
-    }
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) a.s_w[((size_t)g * K + L / 2) * L + sidx_c<L>(tid)] = nyqc[tid];
 #pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) wt_store(CA[u], hvA[u], line + LINES * u);
+    for (int u = 0; u < RG::CPL; ++u) wt_store(CA[u], line + LINES * u);
     GD_TRACE(4);
 #pragma unroll
     for (int q = 0; q < RG::PPL; ++q)
@@ -287,11 +268,8 @@ __global__ __launch_bounds__(512) void k_pois_b(Args a, int init_flag) {
     lds_barrier();  // slice B read -> exchange areas
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
-        f4v hv[F2 / 2];
-        h_load(hv, KS + line + LINES * u);  // under the column FFT
-        __builtin_amdgcn_sched_barrier(0);
         reg_fft<L, false>(CB[u], opaque(j), my, tw);
-        wt_store(CB[u], hv, KS + line + LINES * u);
+        wt_store(CB[u], KS + line + LINES * u);
         __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
