@@ -479,12 +479,11 @@ __device__ __forceinline__ size_t sflat_h(size_t o) {
     else return o;
 }
 // Iteration 0's W~1 = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2) (the first V step, models/
-// Unrolled_ADMM.py:335-336, premultiplied by conj(H); k_col<C_G_W1>'s arithmetic).  At L = 256 it is
-// DEFERRED: the init leaves F(x0) itself in the W~ slot and the first iteration - which reads |H|^2, G
-// and that slot anyway, with rho2 = rho2[0] as the init's - forms W~1 bin by bin (the init then never
-// re-reads |H|^2 and G: 1.5 half spectra per galaxy less).  Other sizes store W~1 in the init.
-template <int L>
-constexpr bool defer_w1() { return L == 256; }
+// Unrolled_ADMM.py:335-336, premultiplied by conj(H); the arithmetic of the reference's first loop body)
+// is DEFERRED at every size: the init leaves F(x0) itself in the W~ slot and the first iteration - which
+// reads |H|^2, G and that slot anyway, with rho2 = rho2[0] - forms W~1 bin by bin.  The init then never
+// re-reads |H|^2 and G (1.5 half spectra per galaxy less) and reads no penalty parameter at all, so it
+// can run while the SubNet computes the rhos (gd_admm_init_reads_rho).
 __device__ __forceinline__ float2 w1_value(float hh, float2 Gk, float2 Xk, float r2n) {
     const float d0 = 1.0f + r2n;
 #if GD_RCP_DIV
@@ -506,7 +505,7 @@ __device__ __forceinline__ GState gauss_load(const Args& a, size_t o) {
     st.hh = ld_s(a.s_hh + sflat_h<L>(o));
     st.G = make_float2(0.f, 0.f);
     st.U1 = make_float2(0.f, 0.f);
-    if constexpr (!LAST || (FIRST && defer_w1<L>())) st.G = ld_s(a.s_g + oc);
+    if constexpr (!LAST || FIRST) st.G = ld_s(a.s_g + oc);
     if constexpr (!FIRST) st.U1 = ld_s(a.s_u1 + oc);
     st.W = ld_s(a.s_w + oc);
     return st;
@@ -552,7 +551,7 @@ __device__ __forceinline__ float2 gauss_iter_st(const Args& a, size_t o, float2 
     const float hh = st.hh;
     const float2 U1 = st.U1, Gk = st.G;
     float2 Wt = st.W;
-    if constexpr (FIRST && defer_w1<L>()) Wt = w1_value(hh, Gk, st.W, r2);  // the slot holds F(x0)
+    if constexpr (FIRST) Wt = w1_value(hh, Gk, st.W, r2);  // the slot holds F(x0)
     const float lhs = r1 * hh + r2;
     const float2 A = csub(Zk, U1);
 #if GD_RCP_DIV
@@ -649,7 +648,7 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     constexpr bool glast = (MODE == C_G_ITER_L || MODE == C_G_ITER_FL);
     const float r1 = (MODE == C_ITER || giter) ? a.rho1(g) : 0.f;
     const float r2 = (MODE == C_ITER || giter) ? a.rho2(g) : 0.f;
-    const float r2n = ((giter && !glast) || MODE == C_G_W1) ? a.rho2n(g) : 0.f;
+    const float r2n = (giter && !glast) ? a.rho2n(g) : 0.f;
 #pragma unroll
     for (int s = 0; s < F2; ++s) {
         const int ky = j + F1 * s;
@@ -692,15 +691,9 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
         } else if constexpr (MODE == C_G_W1) {
             // iteration 0's W~ = conj(H) V1 = (rho2 (|H|^2 X0 + 0) + G) / (1 + rho2): the V step
             // (models/Unrolled_ADMM.py:335-336) with Hx = H X0 and u2 = 0, premultiplied by conj(H)
-            if constexpr (defer_w1<L>()) {
-                // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
-                if (valid)
-                    a.s_w[sflat_c<L>(ob + ky)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(ob + ky)], P[s]) : P[s];
-            } else {
-                const float hh = a.s_hh[sflat_h<L>(ob + ky)];
-                const float2 Gk = a.s_g[sflat_c<L>(ob + ky)];
-                if (valid) a.s_w[sflat_c<L>(ob + ky)] = w1_value(hh, Gk, P[s], r2n);
-            }
+            // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
+            if (valid)
+                a.s_w[sflat_c<L>(ob + ky)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(ob + ky)], P[s]) : P[s];
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
@@ -985,20 +978,14 @@ __device__ __forceinline__ float2 init_bin(const Args& a, size_t o, float2 Yk, f
 }
 // iteration 0's W~ (k_col<C_G_W1>'s arithmetic): the V step (:335-336) with Hx = H X0, u2 = 0, times conj(H)
 template <int L>
-__device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk, float r2n) {
-    if constexpr (defer_w1<L>()) {
-        // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
-        a.s_w[sflat_c<L>(o)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(o)], Xk) : Xk;
-    } else {
-        const float hh = a.s_hh[sflat_h<L>(o)];
-        const float2 Gk = a.s_g[sflat_c<L>(o)];
-        a.s_w[sflat_c<L>(o)] = w1_value(hh, Gk, Xk, r2n);
-    }
+__device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk) {
+    // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
+    a.s_w[sflat_c<L>(o)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(o)], Xk) : Xk;
 }
 template <int L, int KM>
 __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<L>::F2],
                                             const float2 (&Hc)[KM == 1 ? FusedGeo<L>::F2 : 1], int g, int kx, int j,
-                                            float al, float r2n) {
+                                            float al) {
     using FG = FusedGeo<L>;
     constexpr float inv_n = float(1.0 / double(L * L));
     j = opaque(j);
@@ -1010,7 +997,7 @@ __device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<
         if constexpr (KM == 1)
             C[s] = init_bin<L>(a, ob + FG::F1 * s, C[s], Hc[s], al, inv_n);
         else
-            w1_bin<L>(a, ob + FG::F1 * s, C[s], r2n);
+            w1_bin<L>(a, ob + FG::F1 * s, C[s]);
         if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -1026,7 +1013,6 @@ __device__ __forceinline__ void w1_columns(const Args& a, float2 (&X)[FusedGeo<L
     const int line = tid / F1, j = tid - line * F1;
     const bool l0 = (line == 0);
     float2* my = S + line * FG::XCH;
-    const float r2n = a.rho2n(g);
     lds_barrier();  // exchange areas -> slice A
 #pragma unroll
     for (int q = 0; q < FG::PPL; ++q) {
@@ -1088,13 +1074,13 @@ __device__ __forceinline__ void w1_columns(const Args& a, float2 (&X)[FusedGeo<L
     }
     lds_barrier();  // nyqc and slice B complete
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        w1_bin<L>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r2n);
+        w1_bin<L>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid]);
     const float2 dummy[1] = {make_float2(0.f, 0.f)};
-    init_update<L, 2>(a, C, dummy, g, line, j, 1.f, r2n);
+    init_update<L, 2>(a, C, dummy, g, line, j, 1.f);
     fused_gather<L>(S, line, j, C);
     lds_barrier();  // S -> exchange areas
     line_fft<L, false, true>(C, opaque(j), my, tw);
-    init_update<L, 2>(a, C, dummy, g, KS + line, j, 1.f, r2n);
+    init_update<L, 2>(a, C, dummy, g, KS + line, j, 1.f);
 }
 
 template <int L, bool FIRST, bool LAST, int KM = 0>
@@ -1235,7 +1221,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
         fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
     } else {
         unstash<L>(my, C, j);
-        init_update<L, 1>(a, C, Hc, g, line, j, al, r2n);
+        init_update<L, 1>(a, C, Hc, g, line, j, al);
     }
     lds_barrier();  // Nyquist results
 #pragma unroll
@@ -1295,7 +1281,7 @@ __global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
         init_hload<L>(a, Hc, g, KS + line, j);
         init_hfft<L>(Hc, j, false, tw, nyqh);
         unstash<L>(my, Cb, j);
-        init_update<L, 1>(a, Cb, Hc, g, KS + line, j, al, r2n);
+        init_update<L, 1>(a, Cb, Hc, g, KS + line, j, al);
     }
     line_fft<L, true, true>(Cb, opaque(j), my, tw);
 
@@ -1628,6 +1614,9 @@ __device__ __forceinline__ void small_gather(const float2* D, int j, int r, floa
     }
 }
 
+#ifndef GD_SMALL_ZPRE
+#define GD_SMALL_ZPRE 1  // k_gal_small: z's row pair loaded before the twiddles (one pair per line)
+#endif
 // ---------------------------------------------------------------- fused small-image Gaussian iteration
 // L <= 128 (LSST stamps are 48^2): a galaxy's whole half spectrum fits in LDS (9.6 KiB at 48^2, 66.5 KiB
 // at 128^2), so one 256-thread workgroup per galaxy runs the whole iteration on chip - row FFTs of z,
@@ -1646,6 +1635,17 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
     float2* my = xch + line * XCH;
+    GD_TRACE(0);
+    // z's row pair of this line (one pair per line when L / 2 <= LINES), loaded first so that its latency
+    // hides behind the twiddles and the state prefetch
+    constexpr bool ZPRE = GD_SMALL_ZPRE && L / 2 <= LINES;
+    const float* z = a.a0 + (size_t)g * L * L;
+    float2 zv[ZPRE ? F2 : 1];
+    if (ZPRE && line < L / 2) {
+#pragma unroll
+        for (int s = 0; s < (ZPRE ? F2 : 0); ++s)
+            zv[s] = make_float2(z[(2 * line) * L + j + F1 * s], z[(2 * line + 1) * L + j + F1 * s]);
+    }
     fill_twiddles<L>(tw, tid, 256);
     const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
     // the state of this line's first column, loaded now so that its latency hides behind phase R (at
@@ -1658,17 +1658,23 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
         for (int s = 0; s < (PRE ? F2 : 0); ++s) pre[s] = gauss_load<L, FIRST, LAST>(a, ob + F1 * s);
     }
     __syncthreads();
+    GD_TRACE(1);
 
     // R: row pair p -> FFT -> the two rows' half spectra into S (transposed)
-    const float* z = a.a0 + (size_t)g * L * L;
     for (int p = line; p < L / 2; p += LINES) {
         float2 v[F2];
+        if constexpr (ZPRE) {
 #pragma unroll
-        for (int s = 0; s < F2; ++s) v[s] = make_float2(z[(2 * p) * L + j + F1 * s], z[(2 * p + 1) * L + j + F1 * s]);
+            for (int s = 0; s < F2; ++s) v[s] = zv[s];
+        } else {
+#pragma unroll
+            for (int s = 0; s < F2; ++s) v[s] = make_float2(z[(2 * p) * L + j + F1 * s], z[(2 * p + 1) * L + j + F1 * s]);
+        }
         line_fft<L, false>(v, j, my, tw);
         small_split<L>(v, j, my, S, 2 * p);
     }
     __syncthreads();  // all of z read (zin may alias z), S complete
+    GD_TRACE(2);
 
     // C: column kx -> FFT -> spectral update -> IFFT (back in place)
     for (int kx = line; kx < K; kx += LINES) {
@@ -1691,6 +1697,7 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
         for (int s = 0; s < F2; ++s) S[kx * L + j + F1 * s] = v[s];
     }
     __syncthreads();
+    GD_TRACE(3);
 
     // I: Hermitian-extended packed pair spectrum -> inverse row FFT -> zin (x on the last iteration)
     float* out = a.o0 + (size_t)g * L * L;
@@ -1704,28 +1711,35 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
             out[(2 * p + 1) * L + j + F1 * s] = v[s].y;
         }
     }
+    GD_TRACE(4);
 }
 
 // ---------------------------------------------------------------- fused small-image Gaussian init
 // L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
-// G = conj(H) F(max(y,0)/alpha), and iteration 0's W~ = (rho2 |H|^2 X0 + G) / (1 + rho2) (the V step of
-// :207 with u2 = 0, premultiplied by conj(H): k_col<C_G_W1>) in one workgroup per galaxy.  The
-// observation's and the placed PSF's half spectra both fit in LDS (2 x 37.6 KiB at 96^2), so
-// y -> |H|^2, G, X0 -> x0 = clamp(., 0, 1) = zin -> F(x0) -> W~ is one launch instead of
+// G = conj(H) F(max(y,0)/alpha), and F(x0) into the W~ slot (iteration 0 forms W~1 from it, see w1_value)
+// in one workgroup per galaxy.  The observation's and the placed PSF's half spectra both fit in LDS
+// (2 x 37.6 KiB at 96^2), so y -> |H|^2, G, X0 -> x0 = clamp(., 0, 1) = zin -> F(x0) is one launch instead of
 // RF_YA -> psf_rows -> G_INIT -> RIF_CLAMP -> G_W1 through the workspace; same arithmetic as that chain.
-template <int L>
-__global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
-    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1, LINES = 256 / F1, XCH = xch_elems<L>();
+// LDS of the body on NT threads (float2 units): twiddles | S [kx][ky] (row spectra of max(y,0)/alpha ->
+// X0 -> row spectra of x0) | SH [kx][ky] (row spectra of the placed PSF) | the lines' exchange areas
+template <int L, int NT>
+struct SmallInitLds {
+    static constexpr int K = L / 2 + 1, LINES = NT / Plan<L>::F1;
+    static constexpr int TW = 0, S = L, SH = S + K * L, XCH = SH + K * L, SIZE = XCH + LINES * xch_elems<L>();
+};
+template <int L, int NT>
+__device__ __forceinline__ void gal_small_init_body(const Args& a, int g, int tid, float2* lds) {
+    using LY = SmallInitLds<L, NT>;
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1, LINES = LY::LINES, XCH = xch_elems<L>();
     constexpr float inv_n = float(1.0 / double(L * L));
-    __shared__ float2 tw[L];
-    __shared__ float2 S[K * L];   // [kx][ky]: row spectra of max(y,0)/alpha -> X0 -> row spectra of x0
-    __shared__ float2 SH[K * L];  // [kx][ky]: row spectra of the placed PSF
-    __shared__ float2 xch[LINES * XCH];
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
+    float2* tw = lds + LY::TW;
+    float2* S = lds + LY::S;
+    float2* SH = lds + LY::SH;
+    float2* xch = lds + LY::XCH;
+    const int line = tid / F1, j = tid - line * F1;
     float2* my = xch + line * XCH;
-    fill_twiddles<L>(tw, tid, 256);
-    const float al = a.alpha(g), r2 = a.rho2n(g);
+    fill_twiddles<L>(tw, tid, NT);
+    const float al = a.alpha(g);
     __syncthreads();
 
     // R: pairs q < L/2 of max(y,0)/alpha, pairs q >= L/2 of the placed PSF -> row half spectra
@@ -1790,8 +1804,7 @@ __global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
     }
     __syncthreads();
 
-    // C2: F(x0) columns -> iteration 0's W~ (|H|^2 and G re-read: this thread wrote them in C1)
-    const float d0 = 1.0f + r2;
+    // C2: F(x0) columns -> the W~ slot (the first iteration forms W~1 from it: no |H|^2 / G re-read, no rho)
     for (int kx = line; kx < K; kx += LINES) {
         float2 v[F2];
 #pragma unroll
@@ -1799,13 +1812,50 @@ __global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
         line_fft<L, false>(v, j, my, tw);
         const size_t ob = ((size_t)g * K + kx) * L + j;
 #pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const float hh = a.s_hh[ob + F1 * s];
-            const float2 Gk = a.s_g[ob + F1 * s];
-            a.s_w[ob + F1 * s] =
-                make_float2((r2 * (hh * v[s].x + 0.0f) + Gk.x) / d0, (r2 * (hh * v[s].y + 0.0f) + Gk.y) / d0);
-        }
+        for (int s = 0; s < F2; ++s) a.s_w[ob + F1 * s] = v[s];
     }
+}
+template <int L>
+__global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
+    __shared__ float2 lds[SmallInitLds<L, 256>::SIZE];
+    gal_small_init_body<L, 256>(a, blockIdx.x, threadIdx.x, lds);
+}
+
+// The SubNet (k_subnet_rhos_psf) and the fused small init in ONE launch (configs[1]: 256 x 48^2, both a
+// single latency-bound round of workgroups): blocks [0, N) run galaxy b's SubNet, blocks [N, 2N) galaxy
+// b - N's init on the same 512 threads and the same 80 KiB of LDS, so each CU holds one of each and the
+// init's ~12 us hide under the SubNet's ~43 us (as two launches on one stream they ran back to back; on
+// two streams a hipGraph replay still started the SubNet only once the init had drained).  The init reads
+// no rho (iteration 0 forms W~1), so nothing orders the two halves.
+// Block -> (role, galaxy) maps (map): 0 = SubNets in [0, N), inits in [N, 2N); 1 = the two roles alternate
+// in each XCD's arrival order (block b runs on XCD b % 8; its q = b / 8-th arrival there), over a grid of
+// 2 roundup(N, 8); 2 = the roles alternate block by block.  Blocks of galaxies >= N return at once.
+template <int L>
+__global__ __launch_bounds__(subnet::kThreads) void k_subnet_rhos_init(Args a, const float* __restrict__ psf, long long psf_gstride,
+                                                                        int h, const float* __restrict__ params,
+                                                                        const float* __restrict__ mlp,
+                                                                        const float* __restrict__ alpha,
+                                                                        long long alpha_stride, float* __restrict__ rhos,
+                                                                        int n_out, int map) {
+    static_assert(SmallInitLds<L, subnet::kThreads>::SIZE * 8 <= (subnet::kRegionA + subnet::kRegionB) * 4,
+                  "the init's LDS inside the SubNet's");
+    __shared__ __attribute__((aligned(16))) float AB[subnet::kRegionA + subnet::kRegionB];
+    const int b = blockIdx.x;
+    int g, init;
+    if (map == 1) {
+        const int q = b >> 3;
+        g = ((q >> 1) << 3) | (b & 7);
+        init = q & 1;
+    } else if (map == 2) {
+        g = b >> 1;
+        init = b & 1;
+    } else {
+        init = b >= a.N;
+        g = init ? b - a.N : b;
+    }
+    if (g >= a.N) return;  // uniform per block; no barrier crossed
+    if (!init) subnet::rhos_body(psf, psf_gstride, h, params, mlp, alpha, alpha_stride, rhos, n_out, AB, g, threadIdx.x);
+    else gal_small_init_body<L, subnet::kThreads>(a, g, threadIdx.x, reinterpret_cast<float2*>(AB));
 }
 
 // ---------------------------------------------------------------- RI: row inverse + sink
@@ -2234,6 +2284,7 @@ int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per
 // 60.5 vs 75.5 us at 256 x 48^2), else the feature kernel + batched MLP (1024: 173 vs 212 us; 4096: 584 vs
 // 818 us fused - each fused workgroup re-reads the MLP weights, and 129 VGPRs allow one per CU)
 int g_subnet_fused_max = 256;
+int g_sri_map = 0;  // k_subnet_rhos_init's block -> (role, galaxy) map (tools/kbench_small)
 int g_fused_init = 1;  // Gaussian init at 256^2 (+ k_psf_rows<STATE>): 1 = k_gal_reg_init, 2 = k_gal_iter<KM = 1> +
                        // k_gal_w1, 3 = k_gal_iter<KM = 3>; 0 = chunked
 
@@ -2372,7 +2423,7 @@ struct Ops {
                 b.o0 = a.o2;
                 b.t_slot = 1;
                 GD_TRY(Lc::template rif<RIF_CLAMP>(b, st));
-                return Lc::template col<C_G_W1>(b, st);     // F(x0) -> the W~ slot (defer_w1)
+                return Lc::template col<C_G_W1>(b, st);     // F(x0) -> the W~ slot (iteration 0 forms W~1)
             }));
         }
         Args b = a0;
@@ -2577,7 +2628,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r03.2"; }
+const char* gd_engine_rev(void) { return "r03.3"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
@@ -2688,6 +2739,12 @@ int gd_admm_state_layout(int H, int W, int llh) {
     if (llh == GD_LLH_GAUSSIAN) return 1;
     if (llh != GD_LLH_POISSON) return GD_ERR_ARG;
     return pois_two_pass(H, W, llh) ? 2 : 3;
+}
+
+int gd_admm_init_reads_rho(int H, int W, int llh) {
+    if (!gd_supported_size(H, W)) return GD_ERR_UNSUPPORTED;
+    if (llh == GD_LLH_GAUSSIAN) return 0;  // iteration 0 forms W~1 (w1_value)
+    return llh == GD_LLH_POISSON ? 1 : GD_ERR_ARG;
 }
 
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
@@ -2998,6 +3055,38 @@ int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const flo
                        dim3(gd::subnet::kMlpThreads), 0, (hipStream_t)stream, feat, mlp_params, alpha, alpha_stride,
                        rhos, n_out, N);
     return check_launch("k_subnet_mlp");
+}
+
+int gd_admm_init_subnet_supported(int N, int H, int W, int h, int w, int llh, int n_out) {
+    if (llh != GD_LLH_GAUSSIAN || H != W || !(H == 32 || H == 48 || H == 64) || !g_fused) return 0;
+    if (h != w || h < 2 || (h & 1) || h > gd::subnet::kPsfMaxH || h > H) return 0;
+    return N >= 1 && N <= g_subnet_fused_max && n_out >= 1 && n_out <= gd::subnet::kMaxOut;
+}
+
+int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+                        long long alpha_stride, int llh, int N, int H, int W, void* state, float* zin,
+                        const float* params, const float* mlp_params, float* rhos, int n_out, void* ws, void* stream) {
+    GD_TRY(check_shape(N, H, W));
+    GD_TRY(check_psf(h, w, H, W));
+    if (!gd_admm_init_subnet_supported(N, H, W, h, w, llh, n_out))
+        return fail(GD_ERR_UNSUPPORTED, "gd_admm_init_subnet: not fusable here (gd_admm_init_subnet_supported)");
+    Args a = base_args(N, ws, H, W);
+    a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.alpha = GalScalar{alpha, alpha_stride};
+    a.llh = llh;
+    bind_state(a, state, N, H, W, llh);
+    a.o2 = zin;
+    ProfScope ps("op_admm_init_subnet<" + std::to_string(H) + ",0>", (hipStream_t)stream, 1);
+    const int map = g_sri_map;
+    const dim3 grid(map == 1 ? 2 * ((N + 7) / 8 * 8) : 2 * N), block(gd::subnet::kThreads);
+#define GD_SRI_LAUNCH(LL)                                                                                            \
+    hipLaunchKernelGGL(k_subnet_rhos_init<LL>, grid, block, 0, (hipStream_t)stream, a, psf, psf_gstride, h, params, \
+                       mlp_params, alpha, alpha_stride, rhos, n_out, map)
+    if (H == 32) GD_SRI_LAUNCH(32);
+    else if (H == 48) GD_SRI_LAUNCH(48);
+    else GD_SRI_LAUNCH(64);
+#undef GD_SRI_LAUNCH
+    return check_launch("k_subnet_rhos_init");
 }
 
 int gd_subnet_features(const void* otf128_half, const float* params, float* feat, int N, void* stream) {

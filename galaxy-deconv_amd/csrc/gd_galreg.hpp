@@ -118,7 +118,7 @@ __device__ __forceinline__ float2 gauss_bin4(const Args& a, int g, int ky, float
     const float2 Gk = (last && !first) ? make_float2(0.f, 0.f) : a.s_g[cb + pc];
     const float2 U1 = first ? make_float2(0.f, 0.f) : a.s_u1[cb + pc];
     float2 Wt = a.s_w[cb + pc];
-    if (first) Wt = w1_value(hh, Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
+    if (first) Wt = w1_value(hh, Gk, Wt, r2);  // the slot holds F(x0) (w1_value)
     float2 U1n, Wn;
     const float2 r = gauss_math_rt(hh, Gk, U1, Wt, Zk, r1, r2, r2n, inv_n, U1n, Wn, last);
     if (!last) {
@@ -180,7 +180,7 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
                 C[u][4 * q + e] = pois_math(Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt, C[u][4 * q + e],
                                             r1, r2, inv_n, U1n, Wn, last);
             } else {
-                if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (defer_w1)
+                if (first) Wt = w1_value(G[t].h[e], Gk, Wt, r2);  // the slot holds F(x0) (w1_value)
                 C[u][4 * q + e] = gauss_math_rt(G[t].h[e], Gk, make_float2(G[t].u[h][c], G[t].u[h][c + 1]), Wt,
                                                 C[u][4 * q + e], r1, r2, r2n, inv_n, U1n, Wn, last);
             }
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 //   B  the same for slice B
 //   I  per half of the rows: row IFFTs, x0 = clamp(., 0, 1) -> zin, and the clamped rows' FFTs again
 //   W  F(x0)'s columns (slice A, slice B) -> the W~ slot; iteration 0 forms W~1 = (rho2 |H|^2 F(x0) +
-//      G) / (1 + rho2) from it (defer_w1: |H|^2 and G are not re-read here)
+//      G) / (1 + rho2) from it (w1_value: |H|^2 and G are not re-read here, no rho is read)
 // Bytes per galaxy: y, zin (2 img) + |H|^2, G, F(x0) (2.5 half) + the PSF's compact rows (h (L/2 + 1)
 // complex).  No parking, 16-byte state accesses.
 
@@ -552,12 +552,11 @@ __device__ __forceinline__ void init_update4(const Args& a, float2 (&C)[16], con
         }
     }
 }
-// One column of F(x0) (C) into the W~ slot: iteration 0 forms W~1 from it (defer_w1 at 256^2)
+// One column of F(x0) (C) into the W~ slot: iteration 0 forms W~1 from it (w1_value)
 // POIS: H F(x0) instead (pass B<INIT>'s input, as pass A leaves H X for pass B); H is the G slot this
 // thread wrote for the same column in the init's column pass
 template <int L, bool POIS = false>
 __device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16], int g, int kx, int j) {
-    static_assert(defer_w1<L>(), "the fused init defers W~1 to the first iteration");
     j = opaque(j);
     kx = opaque(kx);
     __builtin_amdgcn_sched_barrier(0);
@@ -618,7 +617,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     float2* my = S + line * RG::XCH;
     float2* park = S + RG::XA;
     fill_twiddles<L>(tw, tid, T);
-    const float al = a.alpha(g), r2n = POIS ? 0.f : a.rho2n(g);  // Poisson: pass B<INIT> takes the V step
+    const float al = a.alpha(g);  // no rho: iteration 0 forms W~1 (Poisson: pass B<INIT> takes the V step)
     GD_TRACE(0);
 
     // R: max(y, 0) / alpha (RF_YA), as a multiply by the galaxy's 1/alpha (within an ulp of the division;
@@ -730,7 +729,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         } else {
             lds_barrier();  // nyqc complete
             if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-                w1_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid], r2n);
+                w1_bin<L>(a, ((size_t)g * RG::K + L / 2) * L + tid, nyqc[tid]);
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) w1_update4<L, POIS>(a, CA[u], g, line + LINES * u, j);
         }

@@ -428,9 +428,10 @@ __global__ __launch_bounds__(kThreads) void k_gen_col(Args a, Dims d) {
         } else if constexpr (giter) {
             // the Gaussian iteration on spectra (gauss_math, shared with every specialised kernel)
             const float hh = a.s_hh[o];
-            const float2 Gk = glast ? make_float2(0.f, 0.f) : a.s_g[o];
+            const float2 Gk = (glast && !gfirst) ? make_float2(0.f, 0.f) : a.s_g[o];
             const float2 U1 = gfirst ? make_float2(0.f, 0.f) : a.s_u1[o];
-            const float2 Wt = a.s_w[o];
+            float2 Wt = a.s_w[o];
+            if constexpr (gfirst) Wt = w1_value(hh, Gk, Wt, a.rho2(g));  // the slot holds F(x0)
             float2 U1o, Wo;
             Pv = gauss_math<glast>(hh, Gk, U1, Wt, Pv, a.rho1(g), a.rho2(g), glast ? 0.f : a.rho2n(g), inv_n, U1o, Wo);
             if constexpr (!glast) {
@@ -438,8 +439,9 @@ __global__ __launch_bounds__(kThreads) void k_gen_col(Args a, Dims d) {
                 a.s_w[o] = Wo;
             }
         } else if constexpr (MODE == C_G_W1) {
-            // iteration 0's W~ = conj(H) V1 (the first V step, models/Unrolled_ADMM.py:335-336)
-            a.s_w[o] = w1_value(a.s_hh[o], a.s_g[o], Pv, a.rho2n(g));
+            // F(x0) -> the W~ slot: iteration 0 forms W~ = conj(H) V1 (the first V step,
+            // models/Unrolled_ADMM.py:335-336) from it (w1_value), so the init reads no rho
+            a.s_w[o] = Pv;
         } else if constexpr (MODE == C_WIENER) {
             // models/Wiener.py:16-18: conj(H) F(y) / (|H|^2 + 350/alpha)
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;

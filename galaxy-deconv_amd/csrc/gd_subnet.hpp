@@ -444,14 +444,12 @@ __global__ __launch_bounds__(kMlpThreads) void k_subnet_mlp(const float* __restr
 // Cache: at a few hundred galaxies (one workgroup per CU) that costs ~2 us per galaxy, against a separate
 // batched launch of 32 workgroups (18 us at 256 x 48^2).
 static_assert(kThreads == kMlpThreads, "the fused kernel runs the MLP with the feature kernel's threads");
-__global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __restrict__ psf, long long psf_gstride,
-                                                             int h, const float* __restrict__ params,
-                                                             const float* __restrict__ mlp,
-                                                             const float* __restrict__ alpha, long long alpha_stride,
-                                                             float* __restrict__ rhos, int n_out, int N) {
-    __shared__ __attribute__((aligned(16))) float AB[kRegionA + kRegionB];
-    const int g = blockIdx.x, tid = threadIdx.x;
-    if (g >= N) return;  // uniform per block; no barrier crossed
+// The kernels pass their own __restrict__ pointer arguments (read-only weights through a struct member
+// lose the no-alias proof that lets them be scalar loads: the SubNet ran 43 -> 58 us at 256 that way).
+__device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long long psf_gstride, int h,
+                                          const float* __restrict__ params, const float* __restrict__ mlp,
+                                          const float* __restrict__ alpha, long long alpha_stride,
+                                          float* __restrict__ rhos, int n_out, float* AB, int g, int tid) {
     psf_pool(psf + (long long)g * psf_gstride, h, AB, tid);
     float* X = AB;                 // features [1024] (region A is free once layer 6 has been read)
     float* P = AB + kRegionA;      // partial sums [8][64], then h1, h2 (region B, after layer 7 read it)
@@ -501,6 +499,16 @@ __global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __res
         }
     }
     SN_TRACE(11);
+}
+__global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __restrict__ psf, long long psf_gstride,
+                                                             int h, const float* __restrict__ params,
+                                                             const float* __restrict__ mlp,
+                                                             const float* __restrict__ alpha, long long alpha_stride,
+                                                             float* __restrict__ rhos, int n_out, int N) {
+    __shared__ __attribute__((aligned(16))) float AB[kRegionA + kRegionB];
+    const int g = blockIdx.x;
+    if (g >= N) return;  // uniform per block; no barrier crossed
+    rhos_body(psf, psf_gstride, h, params, mlp, alpha, alpha_stride, rhos, n_out, AB, g, threadIdx.x);
 }
 
 }  // namespace subnet

@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before dlopen of the engin
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgdeconv.so")
 
 GD_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 GD_LLH = {"Gaussian": 0, "Poisson": 1}
 
 _P = ctypes.c_void_p
@@ -36,6 +36,7 @@ SIGNATURES = {
     "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_admm_state_bytes": (_SZ, [_I, _I, _I, _I]),
     "gd_admm_state_layout": (_I, [_I, _I, _I]),
+    "gd_admm_init_reads_rho": (_I, [_I, _I, _I]),
     "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P]),
     "gd_admm_iter": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P,
                           _P]),
@@ -60,6 +61,8 @@ SIGNATURES = {
     "gd_subnet_mlp_param_count": (_I, [_I]),
     "gd_subnet_rhos": (_I, [_P, _P, _P, _P, _LL, _P, _P, _I, _I, _P]),
     "gd_subnet_rhos_psf": (_I, [_P, _LL, _I, _P, _P, _P, _LL, _P, _P, _I, _I, _P]),
+    "gd_admm_init_subnet_supported": (_I, [_I, _I, _I, _I, _I, _I, _I]),
+    "gd_admm_init_subnet": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P]),
     "gd_profile_enable": (_I, [_I]),
     "gd_profile_collect": (_I, []),
     "gd_profile_get": (_I, [_I, ctypes.c_char_p, _I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_LL)]),

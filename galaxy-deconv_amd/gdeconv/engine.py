@@ -562,6 +562,15 @@ class ADMMState:
         self._dev_index = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
         self.layout = None
         self.iter = 0
+        self._side = None   # the side stream an init_concurrent() is running on, until joined
+        key = (self.H, self.W, self.llh)
+        r = ADMMState._reads_rho.get(key)
+        if r is None:
+            r = ADMMState._reads_rho[key] = int(self.lib.gd_admm_init_reads_rho(self.H, self.W, self.llh))
+        self.init_reads_rho = r > 0
+
+    _reads_rho = {}     # (H, W, llh) -> gd_admm_init_reads_rho
+    _side_streams = {}  # device index -> the side stream init_concurrent forks onto (created once)
 
     @property
     def otf(self):
@@ -574,8 +583,13 @@ class ADMMState:
 
     def init(self, rho2_first):
         """models/Unrolled_ADMM.py:181-196 + init_l2 + the first V step; ``rho2_first`` = (tensor or
-        device pointer, stride)."""
-        r2, r2s = _scalar_arg(rho2_first, self.dev)
+        device pointer, stride), or None when the init reads no rho (``init_reads_rho`` False: Gaussian)."""
+        if rho2_first is None:
+            if self.init_reads_rho:
+                raise ValueError("this init takes the first V step: it needs rho2_first")
+            r2, r2s = None, 0
+        else:
+            r2, r2s = _scalar_arg(rho2_first, self.dev)
         k = self.psf
         yp, ap, as_, sp, wp = self._fixed
         with _on(self.dev):
@@ -585,12 +599,63 @@ class ADMMState:
         self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
         self.iter = 0
 
+    def init_with_subnet(self, params, mlp_params, n_out):
+        """``init`` and the engine SubNet (``subnet_rhos_psf`` of this state's PSFs and alphas; packs from
+        ``SubNet.engine_packs``) in ONE launch (gd_admm_init_subnet: small stamps, small batches, Gaussian)
+        -> the rhos [N, n_out], bit-identical to the two separate calls; None when the pair is not fusable
+        here (the caller then runs the SubNet and ``init`` / ``init_concurrent``)."""
+        if self.init_reads_rho:
+            return None
+        k = self.psf
+        if not self.lib.gd_admm_init_subnet_supported(self.N, self.H, self.W, k.shape[2], k.shape[3], self.llh,
+                                                      int(n_out)):
+            return None
+        if params.numel() != _subnet_param_count() or params.dtype != torch.float32 or params.device != self.dev:
+            raise ValueError("bad SubNet parameter pack")
+        if mlp_params.numel() != _mlp_param_count(int(n_out)) or mlp_params.dtype != torch.float32 \
+                or mlp_params.device != self.dev:
+            raise ValueError("bad SubNet MLP parameter pack")
+        yp, ap, as_, sp, wp = self._fixed
+        with _on(self.dev):
+            rhos = torch.empty(self.N, int(n_out), dtype=torch.float32, device=self.dev)
+            _lib.check(self.lib.gd_admm_init_subnet(
+                yp, k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], ap, as_, self.llh, self.N, self.H, self.W, sp,
+                self.zin.data_ptr(), params.contiguous().data_ptr(), mlp_params.contiguous().data_ptr(),
+                rhos.data_ptr(), int(n_out), wp, _stream(self.dev)), "gd_admm_init_subnet")
+        self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
+        self.iter = 0
+        return rhos
+
+    def init_concurrent(self):
+        """The init (Gaussian: it reads no rho) on a side stream forked from the device's current
+        stream, so that it runs while the caller enqueues the SubNet on the current stream (at 48^2 both
+        are one latency-bound round of workgroups that fit on a CU together).  The first ``step`` (or
+        ``join``) makes the current stream wait for it; graph-capturable (event fork / join)."""
+        if self.init_reads_rho:
+            raise ValueError("this init takes the first V step: it needs the rhos (use init(rho2_first))")
+        main = torch.cuda.current_stream(self.dev)
+        side = ADMMState._side_streams.get(self._dev_index)
+        if side is None:
+            side = ADMMState._side_streams[self._dev_index] = torch.cuda.Stream(device=self.dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.init(None)
+        self._side = side
+
+    def join(self):
+        """Make the device's current stream wait for an ``init_concurrent`` (no-op otherwise)."""
+        if self._side is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self._side)
+            self._side = None
+
     def step(self, z, rho1, rho2, rho2_next, out=None):
         """One loop body (models/Unrolled_ADMM.py:207-213) after the denoiser returned ``z``.
         ``rho*`` are (tensor or device pointer, stride) pairs (``RhoSchedule`` items); ``rho2_next`` None
         marks the last iteration, whose x (times alpha for Poisson) goes to ``out``."""
         if self.layout is None:
             raise _lib.EngineError("ADMMState.step before init")
+        if self._side is not None:
+            self.join()
         if z.dtype != torch.float32 or not z.is_contiguous():
             z = z.float().contiguous()
         if z.shape != self.y.shape:

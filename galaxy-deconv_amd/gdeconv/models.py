@@ -32,6 +32,9 @@ from . import engine
 from .nets import SubNet, XDenseUNet, ZUpdateResUNet, ZUpdateXDenseUNet
 
 
+CONCURRENT_INIT_PIXELS = 1 << 23  # batch pixels from which the Gaussian init overlaps the SubNet
+
+
 class Unrolled_ADMM(nn.Module):
     def __init__(self, n_iters=8, llh="Poisson", denoiser="ResUNet", PnP=True, subnet=True):
         super().__init__()
@@ -78,17 +81,37 @@ class Unrolled_ADMM(nn.Module):
 
     def _forward(self, y, kernel, alpha):
         N = y.shape[0]
-        rho1_iters, rho2_iters = self.rhos(kernel, alpha)
-        st = engine.ADMMState(y, kernel, alpha, self.llh)
         n = self.n
         if n == 0:
+            st = engine.ADMMState(y, kernel, alpha, self.llh)
             with torch.no_grad():
                 zero = torch.zeros(1, device=y.device)
                 st.init((zero, 0))
             return st.zin * st.alpha.view(-1, 1, 1, 1) if self.llh == "Poisson" else st.zin
+        st = engine.ADMMState(y, kernel, alpha, self.llh)
+        rhos = None
+        if self.subnet and "rhos" not in self.__dict__ and not st.init_reads_rho:
+            # Gaussian: the init reads no rho.  Small stamps / batches (configs[1]): the SubNet and the init
+            # in ONE launch whose workgroups share the CUs (gd_admm_init_subnet)
+            packs = self.init.engine_packs(kernel)
+            if packs is not None:
+                rhos = st.init_with_subnet(*packs, self.init.n_out)
+        if rhos is not None:
+            rho1_iters, rho2_iters = self.init.split_rhos(rhos)
+            done = True
+        else:
+            # large batches: the init on a side stream while the SubNet computes the rhos (4096 x 256^2: the
+            # 0.4 ms SubNet hides behind the 1.4 ms init); below that a cross-queue join (~10 us) costs more
+            # than it hides (256 x 48^2 kernel trace: a hipGraph replay started the SubNet only once the
+            # 12 us init had drained)
+            done = self.subnet and not st.init_reads_rho and N * st.H * st.W >= CONCURRENT_INIT_PIXELS
+            if done:
+                st.init_concurrent()
+            rho1_iters, rho2_iters = self.rhos(kernel, alpha)
         r1 = engine.RhoSchedule(rho1_iters, N, st.dev)   # (pointer, stride) per iteration, computed once
         r2 = engine.RhoSchedule(rho2_iters, N, st.dev)
-        st.init(r2[0])
+        if not done:
+            st.init(r2[0])
         out = torch.empty_like(st.y)
         for it in range(n):
             z = self.Z(st.zin)

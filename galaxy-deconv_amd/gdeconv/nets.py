@@ -270,6 +270,28 @@ class SubNet(nn.Module):
                 m.fold_bn = bool(on)
         return self
 
+    def engine_packs(self, kernel):
+        """(conv pack, MLP pack) on the kernel's device when this call can run the whole SubNet on the
+        engine from the PSFs (eval, ROCm, even square PSF of side <= 64, MLP of <= 64 outputs and no
+        autograd into it) - what ``Unrolled_ADMM`` hands to ``ADMMState.init_with_subnet``; else None."""
+        from . import engine
+        if not self._engine_ok(kernel) or kernel.shape[-1] > 64 or not engine.mlp_supported(self.n_out):
+            return None
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters()):
+            return None
+        cpack, mpack = self._engine_pack()
+        if cpack.device != kernel.device:
+            cpack, mpack = cpack.to(kernel.device), mpack.to(kernel.device)
+        return cpack, mpack
+
+    def split_rhos(self, out):
+        """[N, n_out] MLP output -> the forward's return value (rho1, rho2 halves, or the single rho)."""
+        N = out.shape[0]
+        out = out.view(N, 1, self.n_out)
+        if self.n_out == self.n:
+            return out.view(N, 1, 1, self.n)
+        return out[:, :, 0:self.n].view(N, 1, 1, self.n), out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
+
     def forward(self, kernel, alpha):
         N, _, h, w = kernel.shape
         if self._engine_ok(kernel):
@@ -285,13 +307,11 @@ class SubNet(nn.Module):
             mlp_ok = engine.mlp_supported(self.n_out)  # k_subnet_mlp: n_out <= 64 (kMaxOut)
             if mlp_ok and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters())):
                 if h <= 64:  # |FFT2(pad128(psf))|^2 inside the feature kernel (no OTF128 pre-pass)
-                    out = engine.subnet_rhos_psf(kernel, cpack, mpack, alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
+                    out = engine.subnet_rhos_psf(kernel, cpack, mpack, alpha.reshape(-1), self.n_out)
                 else:
                     out = engine.subnet_rhos(engine.psf_to_otf_half(kernel, N, 128, 128), cpack, mpack,
-                                             alpha.reshape(-1), self.n_out).view(N, 1, self.n_out)
-                if self.n_out == self.n:
-                    return out.view(N, 1, 1, self.n)
-                return out[:, :, 0:self.n].view(N, 1, 1, self.n), out[:, :, self.n:2 * self.n].view(N, 1, 1, self.n)
+                                             alpha.reshape(-1), self.n_out)
+                return self.split_rhos(out)
             feat = engine.subnet_features(engine.psf_to_otf_half(kernel, N, 128, 128), cpack)
         else:
             h1, h2 = (128 - h) // 2, 128 - h - (128 - h) // 2

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define GD_ABI_VERSION 3
+#define GD_ABI_VERSION 4
 
 #define GD_OK 0
 #define GD_ERR_ARG (-1)
@@ -88,7 +88,10 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
  * (gd_workspace_bytes) is scratch for the duration of one call only.
  *
  * gd_admm_init: OTF, x0 = clamp(init_l2) -> zin (the first denoiser input, x0 + u1 with u1 = 0),
- *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].
+ *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].  llh = Gaussian: the
+ *               first V step is formed by iteration 0 (gd_admm_iter's rho2 is rho2_iters[..., 0]), so
+ *               the init reads no rho (rho2 may be NULL) and may run while the SubNet computes the
+ *               schedule (gd_admm_init_reads_rho).
  * gd_admm_iter: one loop body after the denoiser produced z from zin (iter = 0-based index):
  *               X update, duals, then (unless last) the next V step with rho2_next and the next
  *               denoiser input x + u1 -> zin_or_out; last != 0 -> zin_or_out = x (times alpha for
@@ -100,6 +103,9 @@ size_t gd_admm_state_bytes(int N, int H, int W, int llh);
  * gd_set_fused_iteration, so a caller records it at init and checks it before each gd_admm_iter (a
  * toggle in between would bind a different layout than the init wrote). */
 int gd_admm_state_layout(int H, int W, int llh);
+/* 1 if gd_admm_init reads its rho2 argument for (H, W, llh) (Poisson: the first V step is taken in
+ * the init), 0 if it does not (Gaussian, every size), negative = unsupported. */
+int gd_admm_init_reads_rho(int H, int W, int llh);
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
                  int llh, int N, int H, int W, void* state, float* zin, void* ws, void* stream);
@@ -183,6 +189,17 @@ int gd_subnet_rhos(const void* otf128_half, const float* params, const float* ml
 int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const float* params, const float* mlp_params,
                        const float* alpha, long long alpha_stride, float* feat, float* rhos, int n_out, int N,
                        void* stream);
+
+/* gd_admm_init (llh = Gaussian) and gd_subnet_rhos_psf of the same batch in ONE launch: the SubNet's
+ * workgroups and the init's share the CUs (models/Unrolled_ADMM.py:177-196, the rhos of :77-90 and
+ * init_l2 :170-175; the Gaussian init reads no rho, so the two are independent).  For small square
+ * images (32, 48, 64: the LSST stamps of configs[1]) and batches of at most the fused-SubNet limit;
+ * gd_admm_init_subnet_supported says whether a call is fusable, otherwise the call returns
+ * GD_ERR_UNSUPPORTED and the caller runs the two entry points.  Results are bit-identical to the pair. */
+int gd_admm_init_subnet_supported(int N, int H, int W, int h, int w, int llh, int n_out);
+int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
+                        long long alpha_stride, int llh, int N, int H, int W, void* state, float* zin,
+                        const float* params, const float* mlp_params, float* rhos, int n_out, void* ws, void* stream);
 
 /* Infinity-Cache pipelining: multi-kernel operations (ADMM init/iteration, Wiener, Richardson-Lucy)
  * run over the batch in chunks of about `bytes` of workspace (default 96 MiB, i.e. 186 galaxies at

@@ -50,7 +50,7 @@ def test_library_exports_every_header_symbol(lib):
 
 def test_host_only_queries(lib):
     from gdeconv import _lib as _lib_mod
-    assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 3
+    assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 4
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
     # other sizes up to 1024 per side, square or not, run the runtime-planned kernels (2)
     assert lib.gd_supported_size(50, 50) == 2 and lib.gd_supported_size(256, 128) == 2
