@@ -211,12 +211,15 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
 #ifndef GD_REG_NOFFT
 #define GD_REG_NOFFT 0
 #endif
+#ifndef GD_REG_LEAN
+#define GD_REG_LEAN 1  // 1: twiddles W^{j k1} synthesised from 6 table entries; 0: 15 table reads
+#endif
 template <int L, bool INV, bool DPP = false>
 __device__ __forceinline__ void reg_fft(float2 (&v)[16], int j, float2* xch, const float2* tw) {
 #if GD_REG_NOFFT
     asm volatile("" ::: "memory");
 #else
-    line_fft<L, INV, true, DPP>(v, j, xch, tw);
+    line_fft<L, INV, GD_REG_LEAN != 0, DPP>(v, j, xch, tw);
 #endif
 }
 

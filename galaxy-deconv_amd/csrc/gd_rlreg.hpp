@@ -17,6 +17,9 @@
 #ifndef GD_RL_SRC_EARLY
 #define GD_RL_SRC_EARLY 0  // 1: the row pass loads y / x before the row IFFT (52 VGPRs spilled: slower)
 #endif
+#ifndef GD_RL_HPF
+#define GD_RL_HPF 0  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden)
+#endif
 #ifndef GD_RL_FASTDIV
 #define GD_RL_FASTDIV 1
 #endif
@@ -102,13 +105,19 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
         // column transformed, multiplied by H (CONJ: conj H) / L^2 and transformed back
         auto cols = [&](auto conjc) {
             constexpr bool CONJ = decltype(conjc)::value;
-            auto hmul = [&](float2 (&C)[F2], int kx) {
+            auto hload = [&](float2 (&h)[F2], int kx) {
                 const float2* Hc = Hg + (size_t)opaque(kx) * L + opaque(j);
-                float2 h[F2];
 #pragma unroll
                 for (int s = 0; s < F2; ++s) h[s] = Hc[F1 * s];
+            };
+            auto happly = [&](float2 (&C)[F2], const float2 (&h)[F2]) {
 #pragma unroll
                 for (int s = 0; s < F2; ++s) C[s] = cscale(CONJ ? cmulc(C[s], h[s]) : cmul(C[s], h[s]), inv_n);
+            };
+            auto hmul = [&](float2 (&C)[F2], int kx) {
+                float2 h[F2];
+                hload(h, kx);
+                happly(C, h);
             };
             lds_barrier();  // exchange areas / row spectra -> slice A
 #pragma unroll
@@ -140,6 +149,12 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #pragma unroll
                 for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tt] = X[q][r];
             __builtin_amdgcn_sched_barrier(0);
+#if GD_RL_HPF & 1
+            float2 hA[RG::CPL][F2];  // slice A's OTF columns in flight during its forward FFTs
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) hload(hA[u], line + LINES * u);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 reg_fft<L, false>(CA[u], opaque(j), my, tw);
@@ -160,7 +175,11 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             }
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
+#if GD_RL_HPF & 1
+                happly(CA[u], hA[u]);
+#else
                 hmul(CA[u], line + LINES * u);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
             }
             lds_barrier();  // nyqc complete
@@ -210,10 +229,20 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #pragma unroll
             for (int s = 0; s < F2; ++s) park[s * T + tt] = CA[RG::CPL - 1][s];
             __builtin_amdgcn_sched_barrier(0);
+#if GD_RL_HPF & 2
+            float2 hB[RG::CPL][F2];  // slice B's OTF columns in flight during its forward FFTs
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) hload(hB[u], KS + line + LINES * u);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 reg_fft<L, false>(CB[u], opaque(j), my, tw);
+#if GD_RL_HPF & 2
+                happly(CB[u], hB[u]);
+#else
                 hmul(CB[u], KS + line + LINES * u);
+#endif
                 reg_fft<L, true>(CB[u], opaque(j), my, tw);
                 pin(CB[u]);
                 __builtin_amdgcn_sched_barrier(0);
