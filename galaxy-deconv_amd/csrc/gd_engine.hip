@@ -87,6 +87,7 @@ struct Args {
     int otf_bcast;         // LOAD_OTF modes: one OTF for every galaxy (conv_fft_batch's broadcast H)
     float2* s_x;           // Poisson two-pass at 256^2: X (pass A -> pass B), state layout as s_u1
     int gH, gW;            // image rows / columns (the runtime-size path, gd_generic.hpp)
+    int pw;                // PSF columns when the PSF is h x pw, not square (0 = h; the runtime-size path)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
@@ -2858,13 +2859,16 @@ namespace {
 int check_gx(int N, int H, int W) {
     if (N < 0) return fail(GD_ERR_ARG, "negative batch");
     // pad_double (utils/utils_torch.py:11-13) doubles even sides only (an odd side gives a 2H - 1 grid
-    // whose crop_half no longer matches the image in the reference)
-    if (H != W || H % 2 || !gd_supported_size(2 * H, 2 * W) || (specialised_size(2 * H, 2 * W) && H % 4))
-        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: square images of even side 2 .. 512 (2x padded grid)");
+    // whose crop_half no longer matches the image in the reference); H != W pads each side on its own
+    // (a 2H x 2W grid: the runtime-planned path, which sizes the padding per axis)
+    if (H % 2 || W % 2 || !gd_supported_size(2 * H, 2 * W) || (specialised_size(2 * H, 2 * W) && H % 4))
+        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: images of even sides 2 .. 512 (2x padded grid)");
     return GD_OK;
 }
-void bind_gx_state(Args& a, void* state, int N, int H) {
-    const size_t spec = (size_t)N * (H + 1) * (2 * H);  // half spectrum of the 2H x 2H grid
+// half spectrum of the 2H x 2W grid, [N][W + 1][2H] (complex elements)
+size_t gx_spec_elems(int N, int H, int W) { return (size_t)N * (W + 1) * (2 * H); }
+void bind_gx_state(Args& a, void* state, int N, int H, int W) {
+    const size_t spec = gx_spec_elems(N, H, W);
     a.s_hh = reinterpret_cast<float*>(state);
     a.s_g = reinterpret_cast<float2*>(state) + spec / 2;
 }
@@ -2872,12 +2876,12 @@ void bind_gx_state(Args& a, void* state, int N, int H) {
 
 size_t gd_gx_state_bytes(int N, int H, int W) {
     if (check_gx(N, H, W) != GD_OK || N <= 0) return 0;
-    return (size_t)N * (H + 1) * (2 * H) * (sizeof(float) + sizeof(float2));
+    return gx_spec_elems(N, H, W) * (sizeof(float) + sizeof(float2));
 }
 
 size_t gd_gx_spec_bytes(int N, int H, int W) {
     if (check_gx(N, H, W) != GD_OK || N <= 0) return 0;
-    return (size_t)N * (H + 1) * (2 * H) * sizeof(float2);
+    return gx_spec_elems(N, H, W) * sizeof(float2);
 }
 
 int gd_gx_init(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
@@ -2887,8 +2891,9 @@ int gd_gx_init(const float* y, const float* psf, long long psf_gstride, int h, i
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, 2 * H, 2 * W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;
+    a.pw = w == h ? 0 : w;  // H x W (non-square: the runtime-planned path places it per axis)
     a.alpha = GalScalar{alpha, alpha_stride};
-    bind_gx_state(a, state, N, H);
+    bind_gx_state(a, state, N, H, W);
     a.o0 = z0;
     return dispatch<Ops>(2 * H, 2 * W, [&](auto op) { return decltype(op)::gx_init(a, (hipStream_t)stream); });
 }
@@ -2900,7 +2905,7 @@ int gd_gx_xupdate(const float* z, float* u, const float* x_prev, const float* rh
     if (x_prev && (!u || !rho_prev)) return fail(GD_ERR_ARG, "the fused dual update needs u and rho_prev");
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, 2 * H, 2 * W);
-    bind_gx_state(a, state, N, H);
+    bind_gx_state(a, state, N, H, W);
     a.a0 = z; a.a1 = u; a.a2 = x_prev; a.o1 = u;
     a.rho1 = GalScalar{rho, rho_stride};
     a.rho2 = GalScalar{rho_prev ? rho_prev : rho, rho_prev ? rho_prev_stride : rho_stride};
@@ -2916,7 +2921,7 @@ int gd_gx_xupdate_backward(const float* grad_x, const float* z, const float* rho
     if (!xspec) return fail(GD_ERR_ARG, "backward needs the forward's saved spectrum");
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, 2 * H, 2 * W);
-    bind_gx_state(a, state, N, H);
+    bind_gx_state(a, state, N, H, W);
     a.a0 = grad_x; a.a1 = z;
     a.rho1 = GalScalar{rho, rho_stride};
     a.s_w = reinterpret_cast<float2*>(const_cast<void*>(xspec));

@@ -222,14 +222,16 @@ __device__ float2* fft_lines(float2* x, float2* y, const Axis& ax, const float2*
 
 // ---------------------------------------------------------------- device: sources and sinks
 // psf_to_otf's placement (utils/utils_torch.py:82-88) on an H x W grid: padded pixel (r, c) holds PSF
-// pixel ((r + h/2) mod H, (c + h/2) mod W) when both are < h, zero elsewhere
+// pixel ((r + h/2) mod H, (c + h/2) mod W) when both are < h, zero elsewhere.  An h x pw PSF (a.pw != 0:
+// UnrolledADMMGaussian's image-size kernel of a non-square image, pad_double + ifftshift at
+// models/unrolled_admm_gaussian.py:122) is centred per axis: column offset pw/2, columns < pw.
 __device__ __forceinline__ float gpsf(const Args& a, int g, int r, int c, int H, int W) {
-    const int c0 = a.h >> 1;
-    int i = r + c0, jj = c + c0;
+    const int pw = a.pw ? a.pw : a.h;
+    int i = r + (a.h >> 1), jj = c + (pw >> 1);
     if (i >= H) i -= H;
     if (jj >= W) jj -= W;
-    if (i >= a.h || jj >= a.h) return 0.0f;
-    return a.psf[(long long)g * a.psf_gstride + (long long)i * a.h + jj];
+    if (i >= a.h || jj >= pw) return 0.0f;
+    return a.psf[(long long)g * a.psf_gstride + (long long)i * pw + jj];
 }
 
 // the row-forward producers of gd_engine.hip's rf_source4, one pixel at a time

@@ -180,8 +180,8 @@ class SubNet(nn.Module):
 
     ``forward(kernel [N,1,h,w], alpha [N,1,1,1]) -> (rho1 [N,1,1,n], rho2 [N,1,1,n])``.
     The PSF is zero-padded (or cropped, for h > 128) to 128x128 with floor/ceil split, exactly as
-    ``F.pad`` does at ``:79-81``; the |FFT|^2 feature runs through torch.fft (hipFFT on the GPU),
-    which is 1 small FFT per forward and is off the hot path.
+    ``F.pad`` does at ``:79-81``.  In eval mode on ROCm the whole SubNet runs on the engine for a PSF
+    of any shape (``_engine_kernel``); the torch.fft path below serves training and CPU tensors.
     """
 
     def __init__(self, n, n_out=None, shift=False):
@@ -259,9 +259,27 @@ class SubNet(nn.Module):
         return self._pack_modules()[2]
 
     def _engine_ok(self, kernel):
+        return (self.use_engine and kernel.is_cuda and not self.training
+                and all(dc.fold_bn for dc in self._double_convs()))
+
+    @staticmethod
+    def _engine_kernel(kernel):
+        """A PSF of any h x w -> an even square one of side <= 128 with the same |FFT2(pad128(.))|^2,
+        which is all the SubNet sees (:79-83): sides above 128 cropped with F.pad's floor / ceil split
+        (negative pads), then zeros appended below / right up to an even square side.  |FFT|^2 is
+        invariant to the circular shift that separates any two placements of the same pixels in the
+        128^2 grid, so the engine's psf_to_otf placement of the result gives the reference's feature
+        map.  Even square PSFs of side <= 128 (every BASELINE config) pass through untouched."""
         h, w = kernel.shape[-2:]
-        return (self.use_engine and kernel.is_cuda and not self.training and h == w and h % 2 == 0
-                and h <= 128 and all(dc.fold_bn for dc in self._double_convs()))
+        if h == w and h % 2 == 0 and h <= 128:
+            return kernel
+        if h > 128 or w > 128:
+            t = -((128 - h) // 2) if h > 128 else 0   # -floor(0.5 (128 - h)): the rows F.pad removes on top
+            l = -((128 - w) // 2) if w > 128 else 0   # noqa: E741
+            kernel = kernel[..., t:t + min(h, 128), l:l + min(w, 128)]
+            h, w = kernel.shape[-2:]
+        s = max(h, w) + (max(h, w) & 1)
+        return F.pad(kernel, (0, s - w, 0, s - h))
 
     def set_fold_bn(self, on):
         """Eval-mode BN folding (default on); off reproduces the reference's op order bit-exactly."""
@@ -275,7 +293,9 @@ class SubNet(nn.Module):
         engine from the PSFs (eval, ROCm, even square PSF of side <= 64, MLP of <= 64 outputs and no
         autograd into it) - what ``Unrolled_ADMM`` hands to ``ADMMState.init_with_subnet``; else None."""
         from . import engine
-        if not self._engine_ok(kernel) or kernel.shape[-1] > 64 or not engine.mlp_supported(self.n_out):
+        h, w = kernel.shape[-2:]
+        if (not self._engine_ok(kernel) or h != w or h % 2 or h > 64
+                or not engine.mlp_supported(self.n_out)):
             return None
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.mlp.parameters()):
             return None
@@ -295,6 +315,8 @@ class SubNet(nn.Module):
     def forward(self, kernel, alpha):
         N, _, h, w = kernel.shape
         if self._engine_ok(kernel):
+            kernel = self._engine_kernel(kernel)
+            h = kernel.shape[-1]
             # HIP path: OTF at 128^2 (|.|^2 is shift invariant, so equal to |FFT2(pad128)|^2), then the
             # conv stack (k_subnet_features) and one batched MLP launch (k_subnet_mlp: MLP, Softplus, + 1e-6)
             # (with autograd on and trainable MLP parameters - training UnrolledADMMGaussian, train.py:41 - the

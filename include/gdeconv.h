@@ -140,10 +140,11 @@ int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, v
 int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
                          void* stream);
 
-/* UnrolledADMMGaussian (the variant train.py trains): images H x W (H = W, even, <= 512) and
- * PSFs of the SAME size, zero-padded to the 2H x 2W grid (pad_double) with the reference's
+/* UnrolledADMMGaussian (the variant train.py trains): images H x W (both even, <= 512, square or not:
+ * a non-square image runs on the runtime-planned kernels) and PSFs of the SAME size, zero-padded per
+ * axis to the 2H x 2W grid (pad_double) with the reference's
  * ifftshift / fftshift / crop_half expressed as origin placement (the shift is a common phase that
- * cancels).  state: gd_gx_state_bytes - |H|^2 and G = F(max(y,0)) conj(H) on the 2H grid, written
+ * cancels).  state: gd_gx_state_bytes - |H|^2 and G = F(max(y,0)) conj(H) on the 2H x 2W grid, written
  * by gd_gx_init, which also writes z0 = init_l2 (H x W).  ws: gd_workspace_bytes(N, 2H, 2W).
  *
  * gd_gx_xupdate: x = XUpdateGaussian(Y, Ht, HtH, z, u, rho) (H x W).  u may be NULL (zero).  If

@@ -58,6 +58,11 @@ def test_host_only_queries(lib):
     # workspace: N * 2 images * (W/2+1) * H complex64
     assert lib.gd_workspace_bytes(4096, 256, 256) == 4096 * 2 * 129 * 256 * 8
     assert lib.gd_otf_bytes(2, 48, 48) == 2 * 25 * 48 * 8
+    # UnrolledADMMGaussian's state on the 2H x 2W grid ([N][W+1][2H] |H|^2 fp32 + conj(H) Y complex64):
+    # even sides, square or not (pad_double per axis); odd sides are unsupported, as in the reference
+    assert lib.gd_gx_state_bytes(2, 40, 56) == 2 * 57 * 80 * 12
+    assert lib.gd_gx_state_bytes(2, 48, 48) == 2 * 49 * 96 * 12
+    assert lib.gd_gx_state_bytes(2, 41, 56) == 0 and lib.gd_gx_state_bytes(2, 40, 513) == 0
 
 
 def test_argument_errors_need_no_device(lib):

@@ -197,6 +197,58 @@ def test_generic_gauss2x_backward(dev):
     assert float(((r.grad.cpu().double() - r64.grad).abs() / r64.grad.abs()).max()) < TOL
 
 
+@pytest.mark.parametrize("H,W", [(40, 56), (48, 30)])
+def test_generic_gauss2x_rect(dev, H, W):
+    """UnrolledADMMGaussian(n=4) with the identity denoiser on a NON-SQUARE image (2H x 2W padded grid,
+    pad_double per axis, models/unrolled_admm_gaussian.py:117-152): the SubNet's rhos, init_l2's z0 and
+    the forward's output against the reference (tests/golden/make_golden_gx_rect.py)."""
+    from gdeconv import engine
+    from gdeconv.weights import make_state_dict
+    from models.unrolled_admm_gaussian import UnrolledADMMGaussian
+    g = golden("gauss2x_rect.npz")
+    t = f"{H}x{W}"
+    obs, psf, alpha = (T(g[f"{t}_{k}"]).to(dev) for k in ("obs", "psf", "alpha"))
+    m = UnrolledADMMGaussian(n_iters=4)
+    m.load_state_dict(make_state_dict(m, 1234))
+    m.Z = torch.nn.Identity()
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        assert nerr(m.init(psf, alpha).cpu().reshape(2, -1), T(g[f"{t}_rho"]).reshape(2, -1)) < TOL
+        st = engine.GaussXState(obs, psf, alpha)
+        assert report(f"UnrolledADMMGaussian init_l2 {t}", st.init().cpu(), T(g[f"{t}_z0"])) < TOL
+        out = m(obs, psf, alpha).cpu()
+    assert report(f"UnrolledADMMGaussian(4) identity {t}", out, T(g[f"{t}_out"])) < TOL
+
+
+def test_generic_gauss2x_rect_backward(dev):
+    """The X update's HIP backward on a non-square 2x grid (30 x 44 -> 60 x 88) against autograd through
+    the fp64 oracle."""
+    from gdeconv import engine
+    from gdeconv.synth import make_batch
+    obs, _, alpha, _ = make_batch(2, 30, 44, h=30, seed=11, device=dev)
+    gen = torch.Generator().manual_seed(6)
+    psf = torch.rand(2, 1, 30, 44, generator=gen).to(dev)
+    psf = psf / psf.sum(dim=(-2, -1), keepdim=True)
+    st = engine.GaussXState(obs, psf, alpha)
+    a, b, u = (torch.randn(obs.shape, generator=gen).to(dev) for _ in range(3))
+    rho = torch.tensor([0.9, 1.6], device=dev).view(2, 1, 1, 1)
+    z = a.clone().requires_grad_(True)
+    r = rho.clone().requires_grad_(True)
+    uu = u.clone().requires_grad_(True)
+    x = engine.gx_x_update(st, z, uu, r)
+    (x * b).sum().backward()
+    _, Y, Ht, HtH = O.gx_spectra(obs.cpu().double(), psf.cpu().double())
+    z64 = a.cpu().double().requires_grad_(True)
+    u64 = u.cpu().double().requires_grad_(True)
+    r64 = rho.cpu().double().requires_grad_(True)
+    x64 = O.gx_x_update(Y, Ht, HtH, z64, u64, r64)
+    assert nerr(x.detach().cpu(), x64.detach()) < TOL
+    (x64 * b.cpu().double()).sum().backward()
+    assert nerr(z.grad.cpu(), z64.grad) < TOL
+    assert nerr(uu.grad.cpu(), u64.grad) < TOL
+    assert float(((r.grad.cpu().double() - r64.grad).abs() / r64.grad.abs()).max()) < TOL
+
+
 def test_generic_batch_invariance_and_odd_batch(dev):
     """Chunked pipeline over a ragged batch at a generic size: every galaxy equals its solo run."""
     from gdeconv import _lib, engine

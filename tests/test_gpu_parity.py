@@ -543,6 +543,32 @@ def test_subnet_rhos_from_psf_matches_otf_path(dev, h):
     assert nerr(a.cpu(), ref.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("h,w", [(47, 47), (40, 56), (33, 20), (100, 72), (130, 130), (150, 91)])
+def test_subnet_any_psf_shape_on_engine(dev, h, w):
+    """Odd, non-square and > 128 PSFs (models/Unrolled_ADMM.py:79-81 pads or crops each axis to 128 with
+    F.pad's floor / ceil split) run the engine SubNet through SubNet._engine_kernel (an even square PSF
+    with the same |FFT2(pad128)|^2): rhos against the PyTorch SubNet in the reference's op order."""
+    from gdeconv.nets import SubNet
+    from gdeconv.weights import make_state_dict
+    net = SubNet(8)
+    net.load_state_dict(make_state_dict(net, 19))
+    net = net.to(dev).eval()
+    N = 5
+    gen = torch.Generator().manual_seed(h * 1000 + w)
+    psf = torch.rand(N, 1, h, w, generator=gen) ** 4
+    psf = (psf / psf.sum(dim=(-2, -1), keepdim=True)).to(dev)
+    alpha = (0.5 + torch.rand(N, 1, 1, 1, generator=gen)).to(dev)
+    k = SubNet._engine_kernel(psf)
+    assert k.shape[-1] == k.shape[-2] and k.shape[-1] % 2 == 0 and k.shape[-1] <= 128
+    with torch.no_grad():
+        r1, r2 = net(psf, alpha)                   # engine path
+        net.set_fold_bn(False)
+        r1_ref, r2_ref = net(psf, alpha)           # PyTorch path (fold off -> engine path off)
+        net.set_fold_bn(True)
+    assert nerr(r1.reshape(N, -1).cpu(), r1_ref.reshape(N, -1).cpu()) < 1e-5
+    assert nerr(r2.reshape(N, -1).cpu(), r2_ref.reshape(N, -1).cpu()) < 1e-5
+
+
 def test_subnet_more_than_32_iterations(dev):
     """n_iters = 40 (80 MLP outputs, beyond the engine MLP's 64): the feature kernel + the PyTorch MLP,
     against the PyTorch SubNet (fold off)."""

@@ -260,6 +260,20 @@ def test_generic_size_full_model_and_gauss2x():
     assert torch.equal(out, T(g["gx_out"]))
 
 
+def test_gauss2x_rect_non_square():
+    """UnrolledADMMGaussian(n=4, identity denoiser) on non-square images (40 x 56, 48 x 30: 2H x 2W grids,
+    tests/golden/make_golden_gx_rect.py): the oracle's init_l2 and forward, bit-exactly."""
+    g = golden("gauss2x_rect.npz")
+    for H, W in g["sizes"]:
+        t = f"{H}x{W}"
+        obs, psf, alpha, rho = T(g[f"{t}_obs"]), T(g[f"{t}_psf"]), T(g[f"{t}_alpha"]), T(g[f"{t}_rho"])
+        _, Y, Ht, HtH = O.gx_spectra(obs, psf)
+        assert torch.equal(O.gx_init_l2(Y, Ht, HtH, alpha), T(g[f"{t}_z0"]))
+        tr = {}
+        out = O.gx_forward(obs, psf, alpha, rho, trace=tr)
+        assert torch.equal(out, T(g[f"{t}_out"]))
+
+
 def test_pixel_max_is_noise_between_two_reference_fft_paths():
     """Why tests/test_gpu_pixel_parity.py bounds the tail (p99, 32nd-largest pixel), not the max, of the floored
     per-pixel error: two equally valid fp32 FFT paths of the reference itself - torch.fft.fftn (the
