@@ -599,6 +599,9 @@ __device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16],
     }
 }
 
+#ifndef GD_INIT_DPP
+#define GD_INIT_DPP 0  // 1: the init's line FFTs transpose in registers (DPP) instead of through the LDS exchange
+#endif
 // POIS: the Poisson two-pass init (k_gal_reg_init<L, true>): the same init_l2 and F(x0), but the OTF
 // itself goes to the G slot (the Poisson V step reads y, not G); pass B then forms w1 and W~1.
 template <int L, bool POIS = false>
@@ -640,7 +643,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < RG::PPL; ++q) {
-        reg_fft<L, false>(X[q], opaque(j), my, tw);
+        reg_fft<L, false, GD_INIT_DPP != 0>(X[q], opaque(j), my, tw);
         pin(X[q]);
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -685,7 +688,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         GD_TRACE(TB + 1);
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
-            reg_fft<L, false>(CA[u], opaque(j), my, tw);
+            reg_fft<L, false, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
             if (POIS) pin(CA[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -721,7 +724,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             }
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, true>(CA[u], opaque(j), my, tw);
+                reg_fft<L, true, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
                 if (POIS) pin(CA[u]);  // the Poisson init: materialised here, spill-free
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -768,7 +771,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
-            reg_fft<L, false>(CB[u], opaque(j), my, tw);
+            reg_fft<L, false, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
             __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 float2 Hc[F2];
                 init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
                 init_update4<L, POIS>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
-                reg_fft<L, true>(CB[u], opaque(j), my, tw);
+                reg_fft<L, true, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
                 if (POIS) pin(CB[u]);
             } else {
                 w1_update4<L, POIS>(a, CB[u], g, KS + line + LINES * u, j);
@@ -835,7 +838,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
             float2 (&V)[F2] = X[2 * hf + w];
-            reg_fft<L, true>(V, opaque(j), my, tw);
+            reg_fft<L, true, GD_INIT_DPP != 0>(V, opaque(j), my, tw);
             float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 o[F1 * r] = V[r].x;
                 o[L + F1 * r] = V[r].y;
             }
-            reg_fft<L, false>(V, opaque(j), my, tw);  // F(x0) rows
+            reg_fft<L, false, GD_INIT_DPP != 0>(V, opaque(j), my, tw);  // F(x0) rows
             pin(V);
             __builtin_amdgcn_sched_barrier(0);
         }

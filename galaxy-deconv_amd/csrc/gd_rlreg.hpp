@@ -20,6 +20,9 @@
 #ifndef GD_RL_HPF
 #define GD_RL_HPF 0  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden)
 #endif
+#ifndef GD_RL_DPP
+#define GD_RL_DPP 0  // 1: every line FFT transposes in registers (DPP) instead of through the LDS exchange
+#endif
 #ifndef GD_RL_FASTDIV
 #define GD_RL_FASTDIV 1
 #endif
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
         float2* my = S + line * RG::XCH;
 #pragma unroll
         for (int q = 0; q < RG::PPL; ++q) {
-            reg_fft<L, false>(X[q], opaque(j), my, tw);
+            reg_fft<L, false, GD_RL_DPP != 0>(X[q], opaque(j), my, tw);
             pin(X[q]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, false>(CA[u], opaque(j), my, tw);
+                reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             }
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, true>(CA[u], opaque(j), my, tw);
+                reg_fft<L, true, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
                 pin(CA[u]);  // the column results materialised here (spill-free register allocation)
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -237,13 +240,13 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, false>(CB[u], opaque(j), my, tw);
+                reg_fft<L, false, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
 #if GD_RL_HPF & 2
                 happly(CB[u], hB[u]);
 #else
                 hmul(CB[u], KS + line + LINES * u);
 #endif
-                reg_fft<L, true>(CB[u], opaque(j), my, tw);
+                reg_fft<L, true, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
                 pin(CB[u]);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #pragma unroll
                         for (int r = 0; r < F2; ++r) src[r] = make_float2(sp[F1 * r], sp[L + F1 * r]);
                     }
-                    reg_fft<L, true>(V, opaque(j), my, tw);
+                    reg_fft<L, true, GD_RL_DPP != 0>(V, opaque(j), my, tw);
                     if (!GD_RL_SRC_EARLY) {
 #pragma unroll
                         for (int r = 0; r < F2; ++r) src[r] = make_float2(sp[F1 * r], sp[L + F1 * r]);
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                             V[r] = make_float2(rl_div(fmaxf(src[r].x, 0.f), V[r].x), rl_div(fmaxf(src[r].y, 0.f), V[r].y));  // y / Hx
                         }
                     }
-                    if (!(UPD && last)) reg_fft<L, false>(V, opaque(j), my, tw);
+                    if (!(UPD && last)) reg_fft<L, false, GD_RL_DPP != 0>(V, opaque(j), my, tw);
                     pin(V);
                     __builtin_amdgcn_sched_barrier(0);
                 }
