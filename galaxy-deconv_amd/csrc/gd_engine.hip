@@ -929,6 +929,31 @@ __device__ __forceinline__ void init_hload(const Args& a, float2 (&Hc)[FusedGeo<
         }
     }
 }
+// init_hload in two halves: the 4 loaded registers (s = 0, 1, F2-2, F2-1) issued early (h4), then the
+// column assembled from them with the compile-time zeros (same values as init_hload)
+template <int L>
+__device__ __forceinline__ void init_hload4(const Args& a, float2 (&h4)[4], int g, int kx, int j) {
+    using FG = FusedGeo<L>;
+    const int h = a.h, c0p = h >> 1;
+    const float2* P0 = a.s_u1 + (size_t)g * FG::K * L + (size_t)opaque(kx) * h;
+    j = opaque(j);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int s = t < 2 ? t : FG::F2 - 4 + t;
+        const int i = (j + FG::F1 * s + c0p) & (L - 1);
+        h4[t] = i < h ? P0[i] : make_float2(0.f, 0.f);
+    }
+}
+template <int L>
+__device__ __forceinline__ void init_hcol(float2 (&Hc)[FusedGeo<L>::F2], const float2 (&h4)[4]) {
+    using FG = FusedGeo<L>;
+#pragma unroll
+    for (int s = 0; s < FG::F2; ++s) Hc[s] = make_float2(0.f, 0.f);
+    Hc[0] = h4[0];
+    Hc[1] = h4[1];
+    Hc[FG::F2 - 2] = h4[2];
+    Hc[FG::F2 - 1] = h4[3];
+}
 // The OTF column's FFT runs with register (DPP) transposes while the data column waits in the line's
 // LDS exchange area (register budget: the two columns are never both in registers).  Line 0 splits
 // the packed columns through nyqh (all reads before any write).

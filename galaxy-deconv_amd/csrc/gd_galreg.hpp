@@ -577,10 +577,17 @@ __device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16],
 }
 // The OTF column kx (FFT'd, LDS exchange) from the PSF's compact row spectra; line 0 (kx = 0, packed
 // with the real Nyquist column) splits it and leaves the Nyquist column's spectrum in nyqh.
+#ifndef GD_INIT_HPF
+#define GD_INIT_HPF 0  // 1: a slice's OTF row values are loaded before its data columns' forward FFTs
+#endif
 template <int L>
 __device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16], int g, int kx, int j, bool l0,
-                                                float2* my, const float2* tw, float2* nyqh) {
-    init_hload<L>(a, Hc, g, kx, j);
+                                                float2* my, const float2* tw, float2* nyqh,
+                                                const float2 (*h4)[4] = nullptr) {
+    if (h4)
+        init_hcol<L>(Hc, *h4);
+    else
+        init_hload<L>(a, Hc, g, kx, j);
     reg_fft<L, false>(Hc, opaque(j), my, tw);
     if (l0) {
 #pragma unroll
@@ -686,6 +693,12 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
         __builtin_amdgcn_sched_barrier(0);
         GD_TRACE(TB + 1);
+        float2 hpA[RG::CPL][4];  // INIT: slice A's OTF row values, in flight during the data columns' FFTs
+        if constexpr (INIT && GD_INIT_HPF && !POIS) {  // (the Poisson init spills with them)
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) init_hload4<L>(a, hpA[u], g, line + LINES * u, j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
@@ -709,7 +722,8 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 float2 Hc[F2];
-                init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh);
+                init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh,
+                                   (GD_INIT_HPF && !POIS) ? &hpA[u] : nullptr);
                 init_update4<L, POIS>(a, CA[u], Hc, g, line + LINES * u, j, ial);
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -769,6 +783,12 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
         }
         __builtin_amdgcn_sched_barrier(0);
+        float2 hpB[RG::CPL][4];  // INIT: slice B's OTF row values, in flight during the data columns' FFTs
+        if constexpr (INIT && GD_INIT_HPF && !POIS) {  // (the Poisson init spills with them)
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) init_hload4<L>(a, hpB[u], g, KS + line + LINES * u, j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
@@ -778,7 +798,8 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
         for (int u = 0; u < RG::CPL; ++u) {
             if constexpr (INIT) {
                 float2 Hc[F2];
-                init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh);
+                init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh,
+                                   (GD_INIT_HPF && !POIS) ? &hpB[u] : nullptr);
                 init_update4<L, POIS>(a, CB[u], Hc, g, KS + line + LINES * u, j, ial);
                 reg_fft<L, true, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
                 if (POIS) pin(CB[u]);
