@@ -1740,6 +1740,120 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
     GD_TRACE(4);
 }
 
+// k_gal_small on a transposing line plan (TP x TQ, more lanes per line than Plan<L>): at 48^2 the 4 x 12
+// plan puts one line on 4 lanes, so each phase is one 48-point transform per thread, a long dependent
+// chain at one wave per SIMD (the launch is one latency-bound round).  8 x 6 spreads a line over 8 lanes
+// (DFT-6 + DFT-8 per lane instead of DFT-12 + 3 DFT-4): forward transforms go (8 lanes x 6 points) ->
+// (6 lanes x 8 points) and the inverses back (tline_fft), so rows load / store and columns read / write
+// S in the 8 x 6 layout and the spectral update runs on the 6 x 8 one.  Same state, same arithmetic per
+// bin (gauss_iter_st) and the same launch contract as k_gal_small.
+#ifndef GD_SMALL_T
+#define GD_SMALL_T 1  // 1: k_gal_small_t<48> (8 x 6) for the 48^2 iteration
+#endif
+template <int L, int TP, int TQ, bool FIRST, bool LAST>
+__global__ __launch_bounds__(256) void k_gal_small_t(Args a) {
+    constexpr int G = TP > TQ ? TP : TQ, K = L / 2 + 1, LINES = 256 / G, XCH = TP * (TQ + 1) > TQ * (TP + 1)
+                                                                               ? TP * (TQ + 1) : TQ * (TP + 1);
+    static_assert(TP * TQ == L && G == TP && XCH >= L + 2 && L / 2 <= LINES && K <= LINES, "one line per thread");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 S[K * L];  // [kx][ky]
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    GD_TRACE(0);
+    // z's row pair of this line, loaded first (its latency hides behind the twiddles and the prefetch)
+    const float* z = a.a0 + (size_t)g * L * L;
+    float2 v[G];
+    if (line < L / 2) {
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * line) * L + j + TP * s], z[(2 * line + 1) * L + j + TP * s]);
+    }
+    fill_twiddles<L>(tw, tid, 256);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    // the state of this line's column (6 x 8 layout: lane j < TQ holds ky = j + TQ k1), loaded now
+    GState pre[TP];
+    const bool cl = line < K && j < TQ;
+    if (cl) {
+        const size_t ob = ((size_t)g * K + line) * L + j;
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) pre[k1] = gauss_load<L, FIRST, LAST>(a, ob + TQ * k1);
+    }
+    __syncthreads();
+    GD_TRACE(1);
+
+    // R: row pair -> FFT -> the two rows' half spectra into S (transposed); the spectrum leaves the
+    // transform in the 6 x 8 layout, written to the line's area in natural order for the split
+    if (line < L / 2) {
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) my[j + TQ * k1] = v[k1];
+        }
+        wave_lds_sync();
+        const int r = 2 * line;
+        for (int k = j; k < K; k += G) {
+            const float2 C = my[k], Dm = my[k == 0 ? 0 : L - k];
+            S[k * L + r] = make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+            S[k * L + r + 1] = make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x));
+        }
+        wave_lds_sync();
+    }
+    __syncthreads();  // all of z read (zin may alias z), S complete
+    GD_TRACE(2);
+
+    // C: column kx -> FFT -> spectral update (6 x 8 layout) -> IFFT (back in place, 8 x 6)
+    if (line < K) {
+        const int kx = line;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) v[s] = S[kx * L + j + TP * s];
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (j < TQ ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1)
+            v[k1] = gauss_iter_st<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], pre[k1], r1, r2, r2n, cl, inv_n);
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) S[kx * L + j + TP * s] = v[s];
+    }
+    __syncthreads();
+    GD_TRACE(3);
+
+    // I: Hermitian-extended packed pair spectrum (6 x 8 layout) -> inverse row FFT -> zin (x last)
+    float* out = a.o0 + (size_t)g * L * L;
+    if (line < L / 2) {
+        const int r = 2 * line;
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) {
+                const int k = j + TQ * k1;
+                const bool self = (k == 0) || (2 * k == L);
+                float2 be, bo;
+                if (2 * k <= L) {
+                    be = S[k * L + r];
+                    bo = S[k * L + r + 1];
+                } else {
+                    be = cconj(S[(L - k) * L + r]);
+                    bo = cconj(S[(L - k) * L + r + 1]);
+                }
+                if (self) {
+                    be.y = 0.f;
+                    bo.y = 0.f;
+                }
+                v[k1] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            out[r * L + j + TP * s] = v[s].x;
+            out[(r + 1) * L + j + TP * s] = v[s].y;
+        }
+    }
+    GD_TRACE(4);
+}
+
 // ---------------------------------------------------------------- fused small-image Gaussian init
 // L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
 // G = conj(H) F(max(y,0)/alpha), and F(x0) into the W~ slot (iteration 0 forms W~1 from it, see w1_value)
@@ -2228,7 +2342,10 @@ struct Launcher {
     template <bool FIRST, bool LAST>
     static int gal_small_v(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kGalSmallName, FIRST + 2 * LAST), st);
-        hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
+        if constexpr (L == 48 && GD_SMALL_T)  // 8 lanes per 48-point line (k_gal_small_t)
+            hipLaunchKernelGGL((k_gal_small_t<L, 8, 6, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
         return check_launch("k_gal_small");
     }
     static int gal_small_init(const Args& a, hipStream_t st) {
@@ -2654,7 +2771,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r03.3"; }
+const char* gd_engine_rev(void) { return "r03.4"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 

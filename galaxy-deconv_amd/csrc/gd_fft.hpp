@@ -267,6 +267,41 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Transposing four-step line FFT, N = P Q on the first max(P, Q) lanes of a line (for plans whose lane
+// count does not divide the points per lane, e.g. 48 = 8 x 6: eight lanes per line instead of four).
+// In: lane j < P holds x[j + P r] in v[r], r < Q.  Out: lane l < Q holds X[l + Q k1] in v[k1], k1 < P.
+// Stage A is a DFT-Q per lane and the twiddle W_N^{j k2}; stage B a DFT-P over the lanes for k2 = l,
+// through the line's LDS area xch (P (Q + 1) float2).  The inverse of a forward (P, Q) transform is
+// tline_fft<N, Q, P, true>, which takes the forward's output layout back to its input layout.  Lanes
+// outside a stage's range compute on don't-care values and never write the exchange area.
+template <int N, int P, int Q, bool INV>
+__device__ __forceinline__ void tline_fft(float2 (&v)[(P > Q ? P : Q)], int j, float2* xch, const float2* tw) {
+    static_assert(P * Q == N, "N = P Q");
+    constexpr int LD = Q + 1;
+    const int ja = j < P ? j : 0, jb = j < Q ? j : 0;
+    c2 x[Q];
+#pragma unroll
+    for (int r = 0; r < Q; ++r) x[r] = tc2(v[r]);
+    DFT<Q, INV>::run(x);
+    c2 t[Q];
+#pragma unroll
+    for (int k2 = 1; k2 < Q; ++k2) t[k2] = pmul_t(x[k2], tc2(tw[ja * k2]));  // ja k2 < N: no wrap
+#pragma unroll
+    for (int k2 = 1; k2 < Q; ++k2) x[k2] = pmul_r<INV>(x[k2], tc2(tw[ja * k2]), t[k2]);
+    if (j < P) {
+#pragma unroll
+        for (int k2 = 0; k2 < Q; ++k2) xch[j * LD + k2] = tf2(x[k2]);
+    }
+    wave_lds_sync();
+    c2 z[P];
+#pragma unroll
+    for (int n1 = 0; n1 < P; ++n1) z[n1] = tc2(xch[n1 * LD + jb]);
+    DFT<P, INV>::run(z);
+#pragma unroll
+    for (int k1 = 0; k1 < P; ++k1) v[k1] = tf2(z[k1]);
+    wave_lds_sync();  // the area may be rewritten by the next transform of this wave
+}
+
 // Twiddle table W_L^m = exp(-2 pi i m / L), m in [0, L), computed in double, rounded once.
 template <int L>
 __device__ __forceinline__ void fill_twiddles(float2* tw, int tid, int nthreads) {

@@ -578,7 +578,7 @@ __device__ __forceinline__ void w1_update4(const Args& a, const float2 (&C)[16],
 // The OTF column kx (FFT'd, LDS exchange) from the PSF's compact row spectra; line 0 (kx = 0, packed
 // with the real Nyquist column) splits it and leaves the Nyquist column's spectrum in nyqh.
 #ifndef GD_INIT_HPF
-#define GD_INIT_HPF 0  // 1: a slice's OTF row values are loaded before its data columns' forward FFTs
+#define GD_INIT_HPF 1  // 1: a slice's OTF row values are loaded before its data columns' forward FFTs
 #endif
 template <int L>
 __device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16], int g, int kx, int j, bool l0,
