@@ -36,6 +36,13 @@ def pretty(kname):
     m = re.search(r"k_gal_small_init<(\d+)>", kname)
     if m:
         return f"k_gal_small_init<{m.group(1)}>"
+    m = re.search(r"k_subnet_rhos_init<(\d+)>", kname)
+    if m:
+        return f"k_subnet_rhos_init<{m.group(1)}>"   # SubNet + the small-image init in one launch
+    m = re.search(r"k_gal_small_t<(\d+), \d+, \d+, (true|false), (true|false)>", kname)
+    if m:  # the transposing-plan small-image iteration: same role (and names) as k_gal_small
+        first, last = m.group(2) == "true", m.group(3) == "true"
+        return f"k_gal_small<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
     m = re.search(r"k_gal_small<(\d+), (true|false), (true|false)>", kname)
     if m:
         first, last = m.group(2) == "true", m.group(3) == "true"
@@ -160,6 +167,11 @@ def main():
             "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in init),
             "launches": out["kernels"][init[-1]]["launches"],
             "note": "fused init: " + " + ".join(init) + ", per call"}
+    if f"k_subnet_rhos_init<{L}>" in out["kernels"]:
+        v = out["kernels"][f"k_subnet_rhos_init<{L}>"]
+        out["kernels"][f"op_admm_init_subnet<{L},Gaussian>"] = {
+            "hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "launches": v["launches"],
+            "note": "SubNet + fused small-image init in one launch (k_subnet_rhos_init), per call"}
     if a.rl_calls:
         tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in out["kernels"].values())
         out["kernels"][f"op_richardson_lucy<{L}>"] = {
