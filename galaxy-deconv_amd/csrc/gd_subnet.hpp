@@ -24,7 +24,7 @@ constexpr int woff(int l) {  // offset of layer l's weights in the packed [w | b
     for (int i = 0; i < l; ++i) o += kCout[i] * kCin[i] * 9 + kCout[i];
     return o;
 }
-constexpr int kParams = woff(8);  // 9,172 floats
+constexpr int kParams = woff(8);  // 9,196 floats
 #ifndef GD_SN_THREADS
 #define GD_SN_THREADS 512  // measured: 256 -> 512 threads per galaxy: 119 -> 74 us at 256 x 48^2, 927 -> 659 us at 4096
 #endif

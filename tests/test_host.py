@@ -129,6 +129,31 @@ def test_subnet_bn_folding_matches_reference_order():
     assert torch.equal(b1, c1)
 
 
+def test_subnet_engine_pack_layout():
+    """The conv pack the engine SubNet kernels read (include/gdeconv.h): per layer the folded weights
+    tap-major [cin][3][3][cout], then the bias [cout] (csrc/gd_subnet.hpp wtap)."""
+    from gdeconv.nets import SubNet, _fold_conv_bn
+    from gdeconv.weights import make_state_dict
+    net = SubNet(4)
+    net.load_state_dict(make_state_dict(net, 3))
+    net.eval()
+    pack = net._packed_params()
+    pairs, _, _ = net._pack_modules()
+    off = 0
+    for conv, bn in pairs:
+        w, b = _fold_conv_bn(conv, bn)
+        co, ci = w.shape[:2]
+        gen = torch.Generator().manual_seed(co * 100 + ci)
+        for _ in range(25):
+            c, i, dy, dx = (int(torch.randint(0, n, (1,), generator=gen)) for n in (co, ci, 3, 3))
+            k = ((i * 3 + dy) * 3 + dx) * co + c
+            assert pack[off + k] == w[c, i, dy, dx]
+        off += co * ci * 9
+        assert torch.equal(pack[off:off + co], b)
+        off += co
+    assert off == pack.numel() == 9196
+
+
 def test_denoiser_micro_batching_is_transparent():
     """ZUpdateResUNet splits large batches into micro-batches (activations of a 4096 x 256^2 batch do
     not fit in HBM); per-galaxy results equal the one-call results (CPU, fp32), with and without
