@@ -61,6 +61,17 @@ constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #ifndef GD_SN_UNROLL_Q
 #define GD_SN_UNROLL_Q 2   // 2 x 2-block layers
 #endif
+// Row stride of the 16^2 stage's activations (layers 3 -> 4 -> 5).  A wave's 64 items are the 8 x 8 blocks
+// of 2 x 2 outputs; with rows of 16 floats the 4 block rows in a 32-lane half start 32 floats apart, so
+// their 4 x 4 window reads (ds_read_b32, bank (a/4) mod 32) hit the same 16 banks: 4-way conflicts.  A
+// stride of 24 puts block rows 16 banks apart: 2-way window reads (the floor for same-parity word reads)
+// and conflict-free float2 stores of layer 4 (rows 2 oy, 2 oy + 1 of a 16-lane group on disjoint banks).
+// One-launch SubNet 41.4-42.0 -> 39.6-39.8 us at 256, batched features 384-387 -> 369-370 us at 4096
+// (20: 40.1-40.3 / 373-375 us), rhos bit-identical (profiles/r03w_subnet_rowstride_ab.txt).
+#ifndef GD_SN_RS16
+#define GD_SN_RS16 24
+#endif
+constexpr int kRS16 = GD_SN_RS16;
 constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
 constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 
@@ -79,7 +90,7 @@ constexpr int csplit(int npix, int cout, int cmax = 64) {
 __device__ __forceinline__ constexpr int wtap(int ci, int dy, int dx, int cout) { return ((ci * 3 + dy) * 3 + dx) * cout; }
 
 // acc[k] = b[c0+k] + sum_ci,dy,dx w[ci][dy][dx][c0+k] in[ci][y+dy-1][x+dx-1]   (zero padding)
-template <int CIN, int COUT, int CPT, int S>
+template <int CIN, int COUT, int CPT, int S, int RSI = S>
 __device__ __forceinline__ void conv_pixel(const float* in, const float* __restrict__ w,
                                            const float* __restrict__ b, int c0, int y, int x, float (&acc)[CPT]) {
 #pragma unroll
@@ -92,7 +103,7 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
                 const int xx = x + dx - 1;
-                const float v = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
+                const float v = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * RSI + xx] : 0.f;
 #pragma unroll
                 for (int k = 0; k < CPT; ++k) acc[k] = fmaf(w[wtap(ci, dy, dx, COUT) + c0 + k], v, acc[k]);
             }
@@ -105,11 +116,13 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
 // item computes the 2 x 2 conv outputs of one block from one 4 x 4 input window, 16 LDS reads per input
 // channel instead of 4 x 9 and 4 CPT independent accumulators.  Every output's fma order (bias, then
 // ci, dy, dx) is conv_pixel's in both forms, so the features do not depend on the form.
-template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL, int CMAX = 64>
+// RSI / RSO: row strides of the input / output activations in LDS (>= S / S'), [c][y][RS]
+template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL, int CMAX = 64, int RSI = S, int RSO = (POOL ? S / 2 : S)>
 __device__ __forceinline__ void conv_layer(const float* in, float* out, const float* __restrict__ w,
                                            const float* __restrict__ b, int tid) {
     static_assert(QUAD || !POOL, "the pooled layers compute 2 x 2 blocks");
     constexpr int SO = POOL ? S / 2 : S;
+    static_assert(RSI >= S && RSO >= SO && RSO % 2 == 0, "row strides");
     constexpr int SI = QUAD ? S / 2 : S;  // work items per row
     constexpr int NITEM = SI * SI;
     constexpr int CS = csplit(NITEM, COUT, CMAX), CPT = COUT / CS;
@@ -132,7 +145,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         const int yy = y0 + r, xx = x0 + c;
-                        win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * S + xx] : 0.f;
+                        win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * RSI + xx] : 0.f;
                     }
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
@@ -148,7 +161,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
             if constexpr (POOL) {
 #pragma unroll
                 for (int k = 0; k < CPT; ++k)  // ReLU outputs are >= 0
-                    out[((c0 + k) * SO + oy) * SO + ox] =
+                    out[((c0 + k) * SO + oy) * RSO + ox] =
                         fmaxf(fmaxf(fmaxf(0.f, acc[0][k]), fmaxf(0.f, acc[1][k])),
                               fmaxf(fmaxf(0.f, acc[2][k]), fmaxf(0.f, acc[3][k])));
             } else {
@@ -156,14 +169,14 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
                 for (int k = 0; k < CPT; ++k)
 #pragma unroll
                     for (int h = 0; h < 2; ++h)
-                        *reinterpret_cast<float2*>(out + ((c0 + k) * S + 2 * oy + h) * S + 2 * ox) =
+                        *reinterpret_cast<float2*>(out + ((c0 + k) * S + 2 * oy + h) * RSO + 2 * ox) =
                             make_float2(fmaxf(acc[2 * h][k], 0.f), fmaxf(acc[2 * h + 1][k], 0.f));
             }
         } else {
             float res[CPT];
-            conv_pixel<CIN, COUT, CPT, S>(in, w, b, c0, oy, ox, res);
+            conv_pixel<CIN, COUT, CPT, S, RSI>(in, w, b, c0, oy, ox, res);
 #pragma unroll
-            for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * SO + ox] = fmaxf(res[k], 0.f);
+            for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * RSO + ox] = fmaxf(res[k], 0.f);
         }
     }
 }
@@ -200,17 +213,18 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
 template <int C5, int C67>
 __device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
     const float* P = params;
-#define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT, CMAX)                                       \
-    conv_layer<CI, CO, S, POOL, QUAD, CMAX>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid); \
+#define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT, CMAX, RSI, RSO)                             \
+    conv_layer<CI, CO, S, POOL, QUAD, CMAX, RSI, RSO>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid); \
     __syncthreads();                                                                             \
     SN_TRACE(3 + l);
-    GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64)   // B[4][64][64]
-    GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64)          // A[4][32][32]   (+ MaxPool of Down(4,8))
-    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64))   // B[8][32][32]
-    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, (C5 < 64 ? GD_SN_CS23 : 64))          // A[8][16][16]   (+ MaxPool of Down(8,16))
-    GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS4 : 64))  // B[16][16][16]
-    GD_SN_LAYER(5, 16, 16, 16, true, true, B, A, C5) // A[16][8][8]    (+ MaxPool of Down(16,16))
-    GD_SN_LAYER(6, 16, 16, 8, false, false, A, B, C67)  // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
+    constexpr int R16 = kRS16;
+    GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64, 64, 64)   // B[4][64][64]
+    GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64, 64, 32)          // A[4][32][32]   (+ MaxPool of Down(4,8))
+    GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64), 32, 32)   // B[8][32][32]
+    GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, (C5 < 64 ? GD_SN_CS23 : 64), 32, R16)         // A[8][16][R16]   (+ MaxPool of Down(8,16))
+    GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS4 : 64), R16, R16) // B[16][16][R16]
+    GD_SN_LAYER(5, 16, 16, 16, true, true, B, A, C5, R16, 8) // A[16][8][8]    (+ MaxPool of Down(16,16))
+    GD_SN_LAYER(6, 16, 16, 8, false, false, A, B, C67, 8, 8)  // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
 #undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
     conv_layer<16, 16, 8, false, false, C67>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
