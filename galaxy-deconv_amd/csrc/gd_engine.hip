@@ -2771,7 +2771,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r03.5"; }
+const char* gd_engine_rev(void) { return "r03.6"; }
 
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 

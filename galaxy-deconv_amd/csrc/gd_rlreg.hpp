@@ -18,7 +18,8 @@
 #define GD_RL_SRC_EARLY 0  // 1: the row pass loads y / x before the row IFFT (52 VGPRs spilled: slower)
 #endif
 #ifndef GD_RL_HPF
-#define GD_RL_HPF 0  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden)
+#define GD_RL_HPF 4  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden);
+                      // bit 2: slice A's column 0 before the FFTs, column 1 right after them; bit 3 (with 2): the Nyquist bins too
 #endif
 #ifndef GD_RL_DPP
 #define GD_RL_DPP 0  // 1: every line FFT transposes in registers (DPP) instead of through the LDS exchange
@@ -158,11 +159,27 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             for (int u = 0; u < RG::CPL; ++u) hload(hA[u], line + LINES * u);
             __builtin_amdgcn_sched_barrier(0);
 #endif
+#if GD_RL_HPF & 4
+            static_assert(RG::CPL == 2, "two columns per line and slice");
+            float2 hA0[F2];  // column 0's OTF, in flight during the FFTs
+            hload(hA0, line);
+#if GD_RL_HPF & 8
+            const bool nq = __builtin_amdgcn_readfirstlane(tt >> 6) < L / 64;
+            float2 hn4 = make_float2(0.f, 0.f);  // the Nyquist bin's OTF too
+            if (nq) hn4 = Hg[(size_t)(L / 2) * L + opaque(tt)];
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
                 reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
                 __builtin_amdgcn_sched_barrier(0);
             }
+#if GD_RL_HPF & 4
+            float2 hA1[F2];  // column 1's OTF, in flight during the split and column 0's products
+            hload(hA1, line + LINES);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
 #pragma unroll
                 for (int s = 0; s < F2; ++s) my[j + F1 * s] = CA[0][s];
@@ -176,6 +193,12 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                 }
                 wave_lds_sync();
             }
+#if GD_RL_HPF & 4
+            happly(CA[0], hA0);
+            __builtin_amdgcn_sched_barrier(0);
+            happly(CA[1], hA1);
+            __builtin_amdgcn_sched_barrier(0);
+#else
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
 #if GD_RL_HPF & 1
@@ -185,9 +208,14 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #endif
                 __builtin_amdgcn_sched_barrier(0);
             }
+#endif
             lds_barrier();  // nyqc complete
             if (__builtin_amdgcn_readfirstlane(tt >> 6) < L / 64) {
+#if GD_RL_HPF & 8
+                const float2 hn = hn4;
+#else
                 const float2 hn = Hg[(size_t)(L / 2) * L + tt];
+#endif
                 nyqc[tt] = cscale(CONJ ? cmulc(nyqc[tt], hn) : cmul(nyqc[tt], hn), inv_n);
             }
             lds_barrier();  // Nyquist products
