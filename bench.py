@@ -301,6 +301,17 @@ def spawn_ranks(args, argv):
     return rc
 
 
+def all_ranks(x, world, backend, dev):
+    """A host float from every rank (all_gather; on the device under RCCL, in host memory under gloo)."""
+    if world == 1:
+        return [float(x)]
+    d = dev if backend == "nccl" else "cpu"
+    t = torch.tensor([float(x)], dtype=torch.float64, device=d)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
 def max_over_ranks(x, world, backend, dev):
     """MAX of a host float over the ranks (on the device under RCCL, in host memory under gloo)."""
     if world == 1:
@@ -380,9 +391,8 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        _lib.profile_reset()
-        # pipelined chunks: time whole operations only (per-launch events would perturb them)
-        _lib.profile_enable(1 if chunk_bytes > 0 else 2)
+        # the timed region: no profiling events (value is the clean rate)
+        _lib.profile_enable(0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -391,11 +401,22 @@ def main():
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
+        assert torch.isfinite(out).all(), "non-finite output"
+        # a separate pass of the same K steps with the library's HIP events on (per operation on the
+        # caller's stream; per launch too when nothing is pipelined): the roofline's launch durations
+        _lib.profile_reset()
+        _lib.profile_enable(1 if chunk_bytes > 0 else 2)
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - tp
         _lib.profile_enable(0)
         kstats = _lib.profile_collect()
-        assert torch.isfinite(out).all(), "non-finite output"
 
-    elapsed = max_over_ranks(t1 - t0, world, backend, dev)
+    rank_times = all_ranks(t1 - t0, world, backend, dev)
+    elapsed = max(rank_times)
     gal_s = N * world * args.steps / elapsed
 
     gather_ms, with_gather = None, None
@@ -408,6 +429,7 @@ def main():
         gather_batch(out, N * world)
         torch.cuda.synchronize()
         gather_ms = max_over_ranks(time.perf_counter() - tg, world, backend, dev) * 1e3
+        gathered_bytes = N * world * out[0].numel() * out.element_size()   # the [N * world, 1, H, W] result
         # ... and overlapped: step k's gather in flight (RCCL's stream) while step k + 1 computes
         with torch.no_grad():
             dist.barrier()
@@ -593,8 +615,19 @@ def main():
                                        "not this engine's traffic (see roofline / kernels.*.algorithmic_bytes_per_call)"},
         "kernels": kernels,
     }
+    rec["profiling_pass"] = {"ms_per_step": tp * 1e3 / args.steps,
+                             "note": "kernels.* and roofline come from a second pass of the same K steps with the "
+                                     "library's HIP events on; value is the event-free timed region"}
+    if world > 1:
+        rec["ranks"] = {"elapsed_s_min": min(rank_times), "elapsed_s_max": max(rank_times),
+                        "spread": max(rank_times) / min(rank_times) - 1.0, "per_rank_galaxies": N}
     if gather_ms is not None:
         rec["gather_ms"] = gather_ms
+        rec["gather"] = {"bytes_per_rank_received": gathered_bytes, "ms": gather_ms,
+                         "GBs_per_rank": gathered_bytes / (gather_ms * 1e-3) / 1e9,
+                         "backend": backend,
+                         "note": "all_gather_into_tensor of every rank's [N, 1, H, W] fp32 output into the whole "
+                                 "batch on every rank (gdeconv.dist.gather_batch)"}
         rec["with_gather"] = with_gather
     if graphed is not None:
         rec["graphed"] = graphed
@@ -624,8 +657,12 @@ def main():
                              "sample": f"{G} galaxies, full model with PyTorch ResUNet (fp32, MIOpen, NHWC), "
                                        f"{args.e2e_forwards} timed forwards after one warm forward"}
         del o2, p2, a2
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if world > 1:
+        dist.barrier()   # every rank's GPU work and collectives are done before rank 0 loads the host cores
+    if rank == 0 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args)
+        if world > 1:
+            rec["cpu_baseline"]["note"] = "rank 0, after every rank's timed and collective work"
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -2773,6 +2773,14 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 // profile is never reported against a different engine
 const char* gd_engine_rev(void) { return "r03.6"; }
 
+// the source hash __graft_entry__.build() computed (gdeconv._lib.source_hash); the "gdsrc:" marker lets the
+// build find it in the binary without loading it
+#ifndef GD_SRC_HASH
+#define GD_SRC_HASH "unknown"
+#endif
+static const char g_src_hash_marker[] = "gdsrc:" GD_SRC_HASH;
+const char* gd_engine_src_hash(void) { return g_src_hash_marker + 6; }
+
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
 int gd_supported_size(int H, int W) {
@@ -2896,6 +2904,8 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     GD_TRY(check_shape(N, H, W));
     GD_TRY(check_psf(h, w, H, W));
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
+    if (llh == GD_LLH_POISSON && rho2 == nullptr)
+        return fail(GD_ERR_ARG, "the Poisson init takes the first V step: it needs rho2");
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, H, W);
     a.y = y; a.psf = psf; a.psf_gstride = psf_gstride; a.h = h;

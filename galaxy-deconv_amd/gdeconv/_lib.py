@@ -25,6 +25,7 @@ _SZ = ctypes.c_size_t
 SIGNATURES = {
     "gd_abi_version": (_I, []),
     "gd_engine_rev": (ctypes.c_char_p, []),
+    "gd_engine_src_hash": (ctypes.c_char_p, []),
     "gd_last_error": (ctypes.c_char_p, []),
     "gd_supported_size": (_I, [_I, _I]),
     "gd_workspace_bytes": (_SZ, [_I, _I, _I]),
@@ -75,6 +76,29 @@ SIGNATURES = {
 }
 
 _lib = None
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def source_files():
+    """The files the engine library is compiled from (the build's dependency list)."""
+    import glob
+    csrc = os.path.join(ROOT, "galaxy-deconv_amd", "csrc")
+    return [os.path.join(csrc, "gd_engine.hip"), *sorted(glob.glob(os.path.join(csrc, "*.hpp"))),
+            os.path.join(ROOT, "include", "gdeconv.h")]
+
+
+def source_hash():
+    """sha256 (first 16 hex digits) over the names and contents of ``source_files()``: what build() compiles
+    into the library (``gd_engine_src_hash``) and smoke() checks against the tree it runs in."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in source_files():
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
 
 
 class EngineError(RuntimeError):
@@ -130,4 +154,4 @@ def check(rc, what):
         raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
 
-__all__ = ["load", "check", "EngineError", "SIGNATURES", "LIB_PATH", "GD_LLH"]
+__all__ = ["load", "check", "EngineError", "SIGNATURES", "LIB_PATH", "GD_LLH", "source_hash", "source_files"]

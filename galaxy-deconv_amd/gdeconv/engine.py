@@ -570,7 +570,7 @@ class ADMMState:
         self.init_reads_rho = r > 0
 
     _reads_rho = {}     # (H, W, llh) -> gd_admm_init_reads_rho
-    _side_streams = {}  # device index -> the side stream init_concurrent forks onto (created once)
+    _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (created once)
 
     @property
     def otf(self):
@@ -634,9 +634,12 @@ class ADMMState:
         if self.init_reads_rho:
             raise ValueError("this init takes the first V step: it needs the rhos (use init(rho2_first))")
         main = torch.cuda.current_stream(self.dev)
-        side = ADMMState._side_streams.get(self._dev_index)
+        # one side stream per (device, caller's stream): two host threads forwarding on their own streams
+        # do not serialise their inits on a shared side stream (nor join each other's)
+        key = (self._dev_index, main.cuda_stream)
+        side = ADMMState._side_streams.get(key)
         if side is None:
-            side = ADMMState._side_streams[self._dev_index] = torch.cuda.Stream(device=self.dev)
+            side = ADMMState._side_streams[key] = torch.cuda.Stream(device=self.dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.init(None)

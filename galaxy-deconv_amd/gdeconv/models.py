@@ -21,7 +21,8 @@ rejected (no CPU path), unsupported reference variants raise instead of misbehav
 ``Unrolled_ADMM`` is inference-only: in training mode its forward raises under autograd when a
 parameter requires grad (the engine writes through raw pointers, so no graph would reach ``self.Z`` /
 ``self.init``; the differentiable variant is ``UnrolledADMMGaussian``, whose X update has a HIP
-backward); in eval mode it runs under ``torch.no_grad()`` and returns an output without a graph.
+backward); in eval mode it runs under ``torch.no_grad()`` and returns an output without a graph (only
+parameter gradients can be dropped that way: an input ``y`` / ``kernel`` / ``alpha`` that requires grad raises).
 """
 import warnings
 
@@ -61,6 +62,12 @@ class Unrolled_ADMM(nn.Module):
         return self.rho1_iters, self.rho2_iters
 
     def forward(self, y, kernel, alpha):
+        if torch.is_grad_enabled() and any(torch.is_tensor(t) and t.requires_grad for t in (y, kernel, alpha)):
+            # the reference's output is differentiable w.r.t. its inputs; the engine's is not: refuse rather
+            # than return an output without the graph the caller asked for
+            raise NotImplementedError(
+                "Unrolled_ADMM on the HIP engine is inference-only: an input requires grad (detach it or call "
+                "under torch.no_grad()); UnrolledADMMGaussian's X update has a HIP backward")
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             if self.training:
                 raise NotImplementedError(
@@ -107,7 +114,13 @@ class Unrolled_ADMM(nn.Module):
             done = self.subnet and not st.init_reads_rho and N * st.H * st.W >= CONCURRENT_INIT_PIXELS
             if done:
                 st.init_concurrent()
-            rho1_iters, rho2_iters = self.rhos(kernel, alpha)
+            try:
+                rho1_iters, rho2_iters = self.rhos(kernel, alpha)
+            except BaseException:
+                # the side-stream init may still be writing st's buffers, which were allocated on the main
+                # stream: join before they return to its pool
+                st.join()
+                raise
         r1 = engine.RhoSchedule(rho1_iters, N, st.dev)   # (pointer, stride) per iteration, computed once
         r2 = engine.RhoSchedule(rho2_iters, N, st.dev)
         if not done:

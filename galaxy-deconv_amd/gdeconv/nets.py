@@ -198,9 +198,22 @@ class SubNet(nn.Module):
                                  nn.Linear(64, 64), nn.ReLU(inplace=True),
                                  nn.Linear(64, self.n_out), nn.Softplus())
 
+    def _module_ids(self):
+        """ids of every module object the engine packs read (the 4 _DoubleConvs, their conv / BN children,
+        the 3 Linear layers): a child replaced in place (``net.mlp[0] = nn.Linear(...)``) changes the key."""
+        ids = [id(self.conv_layers), id(self.mlp)]
+        for down in self.conv_layers._modules.values():
+            dc = down._modules["maxpool_conv"]._modules["1"]
+            seq = dc._modules["double_conv"]._modules
+            ids += (id(dc), id(seq["0"]), id(seq["1"]), id(seq["3"]), id(seq["4"]))
+        m = self.mlp._modules
+        ids += (id(m["0"]), id(m["2"]), id(m["4"]))
+        return tuple(ids)
+
     def _pack_modules(self):
-        """(conv/BN pairs, the 3 Linear layers, the 4 _DoubleConvs), looked up once per module tree."""
-        ident = (id(self.conv_layers), id(self.mlp))
+        """(conv/BN pairs, the 3 Linear layers, the 4 _DoubleConvs), looked up again whenever one of those
+        module objects was replaced."""
+        ident = self._module_ids()
         c = self.__dict__.get("_pmods")
         if c is None or c[0] != ident:
             dcs = [down.maxpool_conv[1] for down in self.conv_layers]

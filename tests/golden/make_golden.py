@@ -98,9 +98,12 @@ def run_admm(obs, psf, alpha, n, llh, identity=False, trace=False):
     return res
 
 
-def main():
+def main(only=None):
+    """``only``: regenerate just that fixture ("otf_conv", "admm48", "admm256_id", "wiener_rl"); the others are
+    left as committed (their arrays are deterministic, but a rewrite changes the zip's timestamps)."""
     torch.manual_seed(0)
     torch.set_num_threads(8)
+    want = (lambda name: only is None or only == name)
 
     # G1: psf_to_otf + conv_fft_batch
     o48, p48, a48 = tutorial()
@@ -113,37 +116,41 @@ def main():
         g1[f"otf{tag}"] = c2r(H[..., : o.shape[-1] // 2 + 1])           # half spectrum
         g1[f"conv_H{tag}"] = conv_fft_batch(H, o).numpy()
         g1[f"conv_Ht{tag}"] = conv_fft_batch(torch.conj(H), o).numpy()
-    np.savez_compressed(os.path.join(HERE, "otf_conv.npz"), **g1)
+    if want("otf_conv"):
+        np.savez_compressed(os.path.join(HERE, "otf_conv.npz"), **g1)
 
     # G2: ADMM at 48^2, N=2 (tutorial + seeded), real ResUNet/SubNet with generated weights
     obs, psf, alpha = batch48()
-    g2 = {"obs": obs.numpy(), "psf": psf.numpy(), "alpha": alpha.numpy()}
-    for llh in ("Gaussian", "Poisson"):
-        for n, tr in ((2, True), (8, llh == "Gaussian")):
-            r = run_admm(obs, psf, alpha, n, llh, trace=tr)
+    g2 = {} if not want("admm48") else {"obs": obs.numpy(), "psf": psf.numpy(), "alpha": alpha.numpy()}
+    for llh in ("Gaussian", "Poisson") if want("admm48") else ():
+        for n in (2, 8):   # per-iteration traces for every (llh, n): Poisson is the reference's default llh
+            r = run_admm(obs, psf, alpha, n, llh, trace=True)
             for k, v in r.items():
                 g2[f"{llh}_n{n}_{k}"] = v
-    np.savez_compressed(os.path.join(HERE, "admm48.npz"), **g2)
+    if want("admm48"):
+        np.savez_compressed(os.path.join(HERE, "admm48.npz"), **g2)
 
     # G3: ADMM spectral engine (denoiser = identity) at 256^2, N=1
     obs, psf, alpha, _ = make_batch(1, 256, seed=3)
     g3 = {"obs": obs.numpy(), "psf": psf.numpy(), "alpha": alpha.numpy()}
-    for llh in ("Gaussian", "Poisson"):
+    for llh in ("Gaussian", "Poisson") if want("admm256_id") else ():
         r = run_admm(obs, psf, alpha, 8, llh, identity=True)
         for k, v in r.items():
             g3[f"{llh}_{k}"] = v
-    np.savez_compressed(os.path.join(HERE, "admm256_id.npz"), **g3)
+    if want("admm256_id"):
+        np.savez_compressed(os.path.join(HERE, "admm256_id.npz"), **g3)
 
     # G4: Wiener and Richardson-Lucy
     g4 = {}
     o1, p1, a1, _ = make_batch(1, 256, seed=5)
-    for tag, (o, p, a) in {"48": batch48(), "256": (o1, p1, a1)}.items():
+    for tag, (o, p, a) in ({"48": batch48(), "256": (o1, p1, a1)} if want("wiener_rl") else {}).items():
         g4[f"obs{tag}"], g4[f"psf{tag}"], g4[f"alpha{tag}"] = o.numpy(), p.numpy(), a.numpy()
         with torch.no_grad():
             g4[f"wiener{tag}"] = Wiener()(o, p, a).numpy()
             for n in (10, 100):
                 g4[f"rl{n}_{tag}"] = Richard_Lucy(n)(o, p).numpy()
-    np.savez_compressed(os.path.join(HERE, "wiener_rl.npz"), **g4)
+    if want("wiener_rl"):
+        np.savez_compressed(os.path.join(HERE, "wiener_rl.npz"), **g4)
 
     m = Unrolled_ADMM(n_iters=8, llh="Gaussian")
     keys = [[k, list(v.shape)] for k, v in m.state_dict().items()]
@@ -154,4 +161,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None)

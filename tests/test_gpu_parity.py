@@ -8,7 +8,7 @@ import pytest
 import torch
 
 import admm_oracle as O
-from conftest import golden
+from conftest import golden, parity_gate
 
 pytestmark = pytest.mark.gpu
 
@@ -113,8 +113,11 @@ def test_richardson_lucy(eng, dev, tag, n):
     g = golden("wiener_rl.npz")
     o, p = T(g["obs" + tag]).to(dev), T(g["psf" + tag]).to(dev)
     from models.Richard_Lucy import Richard_Lucy
-    assert report(f"Richard_Lucy({n}) {tag}^2 (configs[4] at n=100, 256^2)", Richard_Lucy(n)(o, p).cpu(),
-                  T(g[f"rl{n}_{tag}"])) < TOL
+    out = Richard_Lucy(n)(o, p).cpu()
+    report(f"Richard_Lucy({n}) {tag}^2 (configs[4] at n=100, 256^2)", out, T(g[f"rl{n}_{tag}"]))
+    # RL(100) is ill-conditioned (the reference sits ~3e-6 from fp64): engine-limited gate
+    parity_gate(f"Richard_Lucy({n}) {tag}^2", out, T(g[f"rl{n}_{tag}"]),
+                O.richardson_lucy(o.cpu().double(), p.cpu().double(), n))
 
 
 @pytest.mark.parametrize("n", [1, 10])
@@ -282,11 +285,12 @@ def test_small_fused_iteration_matches_three_kernel_path(dev, L, n):
 
 
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
-def test_admm48_replay_reference_denoiser(dev, llh):
+@pytest.mark.parametrize("n", [2, 8])
+def test_admm48_replay_reference_denoiser(dev, llh, n):
     """Feed the reference's own per-iteration denoiser outputs z back in: checks every spectral
-    step of the loop (X, V, duals, next denoiser input x + u1) without the ResUNet in the way."""
+    step of the loop (X, V, duals, next denoiser input x + u1) without the ResUNet in the way; every
+    iteration's denoiser input against the reference's, both llh, n = 2 and 8."""
     g = golden("admm48.npz")
-    n = 2
     obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
     zs, zins = T(g[f"{llh}_n{n}_z"]), T(g[f"{llh}_n{n}_zin"])
     seen = []

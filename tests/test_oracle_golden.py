@@ -245,6 +245,20 @@ def test_generic_sizes_spectral_ops(H, W):
         assert torch.equal(out, T(g[f"{t}_{llh}_out"]))
 
 
+@pytest.mark.parametrize("H,W", [(255, 255), (192, 160)])
+def test_tikhonov_second_lambdas(H, W):
+    """Tikhonov at lam 0.05 / 2.0 on new seeded galaxies (tests/golden/make_golden_tik.py): bit for bit."""
+    torch.set_num_threads(8)
+    g = golden("tik_sizes.npz")
+    t = f"{H}x{W}"
+    obs, psf, alpha = T(g[f"{t}_obs"]), T(g[f"{t}_psf"]), T(g[f"{t}_alpha"])
+    yp = torch.max(obs, torch.zeros_like(obs))
+    for lam in (0.05, 2.0):   # make_golden_tik.LAMS
+        for filt in ("Identity", "Laplacian"):
+            ref = T(g[f"{t}_tik_{filt}_{lam}"])
+            assert torch.equal(O.tikhonov(yp, psf, alpha, torch.tensor(lam), filt), ref), (filt, lam)
+
+
 def test_generic_size_full_model_and_gauss2x():
     """The full Unrolled_ADMM(n=2, 'Gaussian') with the ResUNet at 45 x 60, and UnrolledADMMGaussian(n=4,
     identity denoiser) at 40 x 40 (80 x 80 padded grid)."""
