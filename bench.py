@@ -115,7 +115,9 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
             c = (2 + 6.5 + (2 + 7.5) * (n - 2) + 2 + 4.5) / n
         return 2 * img + c * half
     if k == f"op_admm_init<{L},Gaussian>" and fused:
-        rows = 2 * 2 * h * (L // 2 + 1) * 8 if L == 256 else 0  # k_psf_rows<STATE>'s compact rows, out and in
+        # k_psf_rows<STATE>'s compact row spectra [kx][i] (h (L/2 + 1) complex), written once and read once; the
+        # round-3 model counted them twice over (5.70 GB at 4096 x 256^2 against PMC 5.32 GB = 0.93x; now 5.30 GB)
+        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else 0
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:

@@ -1854,6 +1854,117 @@ __global__ __launch_bounds__(256) void k_gal_small_t(Args a) {
     GD_TRACE(4);
 }
 
+// k_gal_small_t with the row pairs' PACKED spectra in LDS (GD_SMALL_T = 2): the row phase stores each pair's
+// transform as it leaves tline_fft (PR[kx][p], kx in [0, L), no split through the exchange area), the column
+// line kx reads the packed columns kx and L - kx and separates its rows' bins on the fly (the split's
+// arithmetic), and after the inverse column transform it writes the next row phase's packed input for both
+// columns kx and L - kx (the gather's Hermitian extension, bins kx = 0, L/2 real) in place - the columns
+// {kx, L - kx} belong to that line alone, so no barrier separates its reads and writes.  A lane holds rows
+// r = j + TP r' (one parity per lane): the packing pairs lanes j, j ^ 1 through a DPP quad swap.  Per line:
+// R 8 LDS stores instead of 8 + 2 syncs + ~16 split accesses, I 8 reads instead of 16; the same arithmetic
+// per bin as k_gal_small_t, so the outputs are bit-identical to it.
+template <int L, int TP, int TQ, bool FIRST, bool LAST>
+__global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
+    constexpr int G = TP > TQ ? TP : TQ, K = L / 2 + 1, LINES = 256 / G, XCH = TP * (TQ + 1) > TQ * (TP + 1)
+                                                                               ? TP * (TQ + 1) : TQ * (TP + 1);
+    constexpr int SP = L / 2 + 1;  // PR row stride (float2): [kx][p]
+    static_assert(TP * TQ == L && G == TP && TP % 2 == 0 && L / 2 <= LINES && K <= LINES, "one line per thread");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 PR[L * SP];
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    GD_TRACE(0);
+    const float* z = a.a0 + (size_t)g * L * L;
+    float2 v[G];
+    if (line < L / 2) {
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * line) * L + j + TP * s], z[(2 * line + 1) * L + j + TP * s]);
+    }
+    fill_twiddles<L>(tw, tid, 256);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    GState pre[TP];
+    const bool cl = line < K && j < TQ;
+    if (cl) {
+        const size_t ob = ((size_t)g * K + line) * L + j;
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) pre[k1] = gauss_load<L, FIRST, LAST>(a, ob + TQ * k1);
+    }
+    __syncthreads();
+    GD_TRACE(1);
+
+    // R: row pair p = line -> FFT -> its packed spectrum P_p[kx] (6 x 8 layout: lane j < TQ holds kx = j + TQ k1)
+    if (line < L / 2) {
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[(j + TQ * k1) * SP + line] = v[k1];
+        }
+    }
+    __syncthreads();  // all of z read (zin may alias z), PR complete
+    GD_TRACE(2);
+
+    // C: column kx = line: lane j holds rows r = j + TP r' (p = r / 2, parity j & 1) of the column, separated
+    // from the packed columns kx and L - kx as small_split does
+    if (line < K) {
+        const int kx = line, km = kx == 0 ? 0 : L - kx;
+        const bool odd = j & 1;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[kx * SP + p], Dm = PR[km * SP + p];
+            v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (j < TQ ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1)
+            v[k1] = gauss_iter_st<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], pre[k1], r1, r2, r2n, cl, inv_n);
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        // lane j: X_r[kx], r = j + TP s.  Pair rows 2p (even lane) and 2p + 1 (odd lane): the even lane writes
+        // Q_p[kx] = X_2p + i X_2p+1, the odd lane Q_p[L - kx] = conj(X_2p) + i conj(X_2p+1) (small_gather's
+        // arithmetic); the self-conjugate columns kx = 0, L/2 keep real parts only and only the even lane writes
+        const bool self = (kx == 0) || (2 * kx == L);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const float ox = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].x), 0xB1, 0xF, 0xF, false));
+            const float oy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].y), 0xB1, 0xF, 0xF, false));
+            const int p = (j >> 1) + (TP / 2) * s;
+            float2 be = odd ? make_float2(ox, oy) : v[s], bo = odd ? v[s] : make_float2(ox, oy);
+            if (odd) {
+                be = cconj(be);
+                bo = cconj(bo);
+            }
+            if (self) {
+                be.y = 0.f;
+                bo.y = 0.f;
+            }
+            if (!(odd && self)) PR[(odd ? km : kx) * SP + p] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+    }
+    __syncthreads();
+    GD_TRACE(3);
+
+    // I: row pair p's packed spectrum (6 x 8 layout) -> inverse row FFT -> zin (x on the last iteration)
+    float* out = a.o0 + (size_t)g * L * L;
+    if (line < L / 2) {
+        const int r = 2 * line;
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) v[k1] = PR[(j + TQ * k1) * SP + line];
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            out[r * L + j + TP * s] = v[s].x;
+            out[(r + 1) * L + j + TP * s] = v[s].y;
+        }
+    }
+    GD_TRACE(4);
+}
+
 // ---------------------------------------------------------------- fused small-image Gaussian init
 // L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
 // G = conj(H) F(max(y,0)/alpha), and F(x0) into the W~ slot (iteration 0 forms W~1 from it, see w1_value)
@@ -2342,7 +2453,9 @@ struct Launcher {
     template <bool FIRST, bool LAST>
     static int gal_small_v(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kGalSmallName, FIRST + 2 * LAST), st);
-        if constexpr (L == 48 && GD_SMALL_T)  // 8 lanes per 48-point line (k_gal_small_t)
+        if constexpr (L == 48 && GD_SMALL_T == 2)  // packed row spectra in LDS (k_gal_small_p)
+            hipLaunchKernelGGL((k_gal_small_p<L, 8, 6, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
+        else if constexpr (L == 48 && GD_SMALL_T)  // 8 lanes per 48-point line (k_gal_small_t)
             hipLaunchKernelGGL((k_gal_small_t<L, 8, 6, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);

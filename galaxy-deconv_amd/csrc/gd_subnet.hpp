@@ -72,6 +72,10 @@ constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #define GD_SN_RS16 24
 #endif
 constexpr int kRS16 = GD_SN_RS16;
+#ifndef GD_SN_RS8P
+#define GD_SN_RS8P 12  // row stride of the zero-haloed 8^2 stage (10 rows of 10 + pad) on the MFMA path
+#endif
+constexpr int kRS8P = GD_SN_RS8P;
 constexpr int kRegionA = 16 * 16 * 16;  // floats: 64x64x1 input, then pooled stage outputs
 constexpr int kRegionB = 4 * 64 * 64;   // floats: first conv of each stage
 
@@ -117,7 +121,8 @@ __device__ __forceinline__ void conv_pixel(const float* in, const float* __restr
 // channel instead of 4 x 9 and 4 CPT independent accumulators.  Every output's fma order (bias, then
 // ci, dy, dx) is conv_pixel's in both forms, so the features do not depend on the form.
 // RSI / RSO: row strides of the input / output activations in LDS (>= S / S'), [c][y][RS]
-template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL, int CMAX = 64, int RSI = S, int RSO = (POOL ? S / 2 : S)>
+template <int CIN, int COUT, int S, bool POOL, bool QUAD = POOL, int CMAX = 64, int RSI = S, int RSO = (POOL ? S / 2 : S),
+          bool PADO = false>
 __device__ __forceinline__ void conv_layer(const float* in, float* out, const float* __restrict__ w,
                                            const float* __restrict__ b, int tid) {
     static_assert(QUAD || !POOL, "the pooled layers compute 2 x 2 blocks");
@@ -161,7 +166,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
             if constexpr (POOL) {
 #pragma unroll
                 for (int k = 0; k < CPT; ++k)  // ReLU outputs are >= 0
-                    out[((c0 + k) * SO + oy) * RSO + ox] =
+                    out[PADO ? ((c0 + k) * (SO + 2) + oy + 1) * RSO + ox + 1 : ((c0 + k) * SO + oy) * RSO + ox] =
                         fmaxf(fmaxf(fmaxf(0.f, acc[0][k]), fmaxf(0.f, acc[1][k])),
                               fmaxf(fmaxf(0.f, acc[2][k]), fmaxf(0.f, acc[3][k])));
             } else {
@@ -177,6 +182,84 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
             conv_pixel<CIN, COUT, CPT, S, RSI>(in, w, b, c0, oy, ox, res);
 #pragma unroll
             for (int k = 0; k < CPT; ++k) out[((c0 + k) * SO + oy) * RSO + ox] = fmaxf(res[k], 0.f);
+        }
+    }
+}
+
+// ---- the 16-output-channel layers (4, 5, 6, 7) on the matrix cores: v_mfma_f32_16x16x4_f32, an implicit GEMM
+// D[pixel][cout] = bias + sum_k A[pixel][k] W[k][cout] with k = (ci, dy, dx) in conv_pixel's order.  The f32 MFMA
+// is bit for bit a k-ordered fmaf chain (one rounding per product, cdna_hip_programming.md 'FP32-input MFMA'),
+// so every output equals the VALU form's fma(w, v, acc) chain from the bias: the features, and the rhos, are
+// bit-identical to conv_layer's (tests: test_subnet_fused_launch_bit_identical and the rhos against the PyTorch
+// SubNet).  A 16-pixel tile is 4 blocks of 2 x 2 outputs; lane l (q = l >> 4, i = l & 15) holds A[i][4s + q]
+// = the input at pixel i's window offset of k = 4s + q, and W[4s + q][l & 15] (the tap-major weights ARE
+// W[k][cout]: one coalesced load per k-step); its accumulators D[4q + r][l & 15], r < 4, are block q's 2 x 2
+// outputs of channel l & 15, so the 2 x 2 MaxPool is a max over the lane's own registers.  Inputs carry a
+// one-pixel zero halo ([c][S + 2][RSI], interior at (y + 1, x + 1)): no bounds test per tap.  One k-step is
+// one address add, one ds_read_b32 and one MFMA (the VALU form: 16 exec-masked window reads and scalar weight
+// loads per input channel, waited with lgkmcnt(0)).
+#ifndef GD_SN_MFMA
+#define GD_SN_MFMA 1
+#endif
+typedef float sn_f4 __attribute__((ext_vector_type(4)));
+template <int C, int S, int RS>
+__device__ __forceinline__ void zero_halo(float* buf, int tid) {  // [C][S + 2][RS]: rows 0, S + 1 and columns 0, S + 1
+    constexpr int PER = 4 * S + 4;
+    for (int e = tid; e < C * PER; e += kThreads) {
+        const int c = e / PER, u = e - c * PER;
+        int y, x;
+        if (u < S + 2) { y = 0; x = u; }
+        else if (u < 2 * (S + 2)) { y = S + 1; x = u - (S + 2); }
+        else { const int v = u - 2 * (S + 2); y = 1 + (v >> 1); x = (v & 1) ? S + 1 : 0; }
+        buf[(c * (S + 2) + y) * RS + x] = 0.f;
+    }
+}
+// in: [CIN][S + 2][RSI] (zero halo) -> conv3x3 + bias + ReLU (+ MaxPool2d(2) when POOL) ->
+//   OUTF == 0: [16][SO + 2][RSO] with zero halo (SO = S or S / 2; the halo is written here too);
+//   OUTF == 1: the feature vector [16][S][S] (the reference's .view(N, 1, 16 * 8 * 8) order)
+template <int CIN, int S, bool POOL, int RSI, int RSO, int OUTF>
+__device__ __forceinline__ void conv_mfma(const float* in, float* out, const float* __restrict__ w,
+                                          const float* __restrict__ b, int tid) {
+    constexpr int COUT = 16, K = CIN * 9, NS = K / 4, CHI = (S + 2) * RSI, SO = POOL ? S / 2 : S;
+    constexpr int BPR = S / 2, NT = S * S / 16, NW = kThreads / 64;
+    static_assert(K % 4 == 0 && (S * S) % 16 == 0, "k-steps of 4, tiles of 16 pixels");
+    const int wave = tid >> 6, lane = tid & 63, q = lane >> 4, col = lane & 15;
+    if constexpr (OUTF == 0) zero_halo<COUT, SO, RSO>(out, tid);  // disjoint from the interior written below
+    if (wave >= NT) return;  // 8^2 layers: 4 tiles, waves 4-7 idle (no barrier inside)
+    float bw[NS];
+    int off[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int k = 4 * s + q, ci = k / 9, r = k - 9 * ci, dy = r / 3, dx = r - 3 * dy;
+        bw[s] = w[k * COUT + col];
+        off[s] = ci * CHI + dy * RSI + dx;
+    }
+    const float bias = b[col];
+    for (int t = wave; t < NT; t += NW) {
+        // A row of this lane: pixel i = lane & 15 of tile t (block i >> 2, position i & 3)
+        const int ia = lane & 15, blk = 4 * t + (ia >> 2), by = blk / BPR, bx = blk - by * BPR;
+        const int y = 2 * by + ((ia >> 1) & 1), x = 2 * bx + (ia & 1);
+        const float* src = in + y * RSI + x;  // window origin in padded coordinates
+        float av[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) av[s] = src[off[s]];
+        sn_f4 acc = {bias, bias, bias, bias};
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bw[s], acc, 0, 0, 0);
+        // this lane's results: block (t, q), positions r = 0..3 (D row 4q + r), channel col
+        const int ob = 4 * t + q, oby = ob / BPR, obx = ob - oby * BPR;
+        if constexpr (POOL) {
+            const float m = fmaxf(fmaxf(fmaxf(0.f, acc[0]), fmaxf(0.f, acc[1])), fmaxf(fmaxf(0.f, acc[2]), fmaxf(0.f, acc[3])));
+            if constexpr (OUTF == 0) out[(col * (SO + 2) + oby + 1) * RSO + obx + 1] = m;
+            else out[(col * SO + oby) * SO + obx] = m;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int yy = 2 * oby + (r >> 1), xx = 2 * obx + (r & 1);
+                const float v = fmaxf(acc[r], 0.f);
+                if constexpr (OUTF == 0) out[(col * (SO + 2) + yy + 1) * RSO + xx + 1] = v;
+                else out[(col * SO + yy) * SO + xx] = v;
+            }
         }
     }
 }
@@ -221,14 +304,35 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64, 64, 64)   // B[4][64][64]
     GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64, 64, 32)          // A[4][32][32]   (+ MaxPool of Down(4,8))
     GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64), 32, 32)   // B[8][32][32]
+#if GD_SN_MFMA
+    // layer 3 writes the 16^2 stage with a zero halo; layers 4-7 on the matrix cores (conv_mfma)
+    constexpr int P16 = R16, P8 = kRS8P;
+    static_assert(16 * 18 * P16 <= kRegionB && 8 * 18 * P16 <= kRegionA && 16 * 10 * P8 <= kRegionA, "padded stages");
+    zero_halo<8, 16, P16>(A, tid);
+    conv_layer<8, 8, 32, true, true, (C5 < 64 ? GD_SN_CS23 : 64), 32, P16, true>(B, A, P + woff(3), P + woff(3) + 8 * 8 * 9, tid);
+    __syncthreads();
+    SN_TRACE(6);
+    conv_mfma<8, 16, false, P16, P16, 0>(A, B, P + woff(4), P + woff(4) + 16 * 8 * 9, tid);   // B[16][18][P16]
+    __syncthreads();
+    SN_TRACE(7);
+    conv_mfma<16, 16, true, P16, P8, 0>(B, A, P + woff(5), P + woff(5) + 16 * 16 * 9, tid);   // A[16][10][P8]
+    __syncthreads();
+    SN_TRACE(8);
+    conv_mfma<16, 8, false, P8, P8, 0>(A, B, P + woff(6), P + woff(6) + 16 * 16 * 9, tid);     // B[16][10][P8]
+    __syncthreads();
+    SN_TRACE(9);
+    conv_mfma<16, 8, false, P8, P8, 1>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);   // features
+    SN_TRACE(10);
+#else
     GD_SN_LAYER(3, 8, 8, 32, true, true, B, A, (C5 < 64 ? GD_SN_CS23 : 64), 32, R16)         // A[8][16][R16]   (+ MaxPool of Down(8,16))
     GD_SN_LAYER(4, 8, 16, 16, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS4 : 64), R16, R16) // B[16][16][R16]
     GD_SN_LAYER(5, 16, 16, 16, true, true, B, A, C5, R16, 8) // A[16][8][8]    (+ MaxPool of Down(16,16))
     GD_SN_LAYER(6, 16, 16, 8, false, false, A, B, C67, 8, 8)  // B[16][8][8]  (per pixel: 2 x 2 blocks would idle half the threads)
-#undef GD_SN_LAYER
     // last conv of Down(16,16) straight to the feature vector [16][8][8]
     conv_layer<16, 16, 8, false, false, C67>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
     SN_TRACE(10);
+#endif
+#undef GD_SN_LAYER
 }
 
 __global__ __launch_bounds__(kThreads) void k_subnet_features(const float2* __restrict__ otf128,

@@ -5,6 +5,7 @@
 #include "../galaxy-deconv_amd/csrc/gd_engine.hip"
 
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -106,5 +107,16 @@ int main(int argc, char** argv) {
     std::vector<float> hr(n_out);
     CK(hipMemcpy(hr.data(), rhos, n_out * 4, hipMemcpyDeviceToHost));
     printf("rhos[0][:4] = %g %g %g %g\n", hr[0], hr[1], hr[2], hr[3]);
+    // bitwise fingerprints of every feature (batched kernel, N) and every rho (fused kernel, Nr): variants that
+    // must be bit-identical print the same hashes
+    auto fnv = [](const std::vector<float>& v) {
+        unsigned long long h = 1469598103934665603ull;
+        for (float f : v) { unsigned u; memcpy(&u, &f, 4); h = (h ^ u) * 1099511628211ull; }
+        return h;
+    };
+    std::vector<float> hf((size_t)N * 1024), hra((size_t)Nr * n_out);
+    CK(hipMemcpy(hf.data(), feat, hf.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hra.data(), rhos, hra.size() * 4, hipMemcpyDeviceToHost));
+    printf("features fnv %016llx  rhos fnv %016llx\n", fnv(hf), fnv(hra));
     return 0;
 }
