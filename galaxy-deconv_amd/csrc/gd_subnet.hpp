@@ -264,6 +264,84 @@ __device__ __forceinline__ void conv_mfma(const float* in, float* out, const flo
     }
 }
 
+// ---- layers 0-3 (4 / 8 output channels) on v_mfma_f32_4x4x1_16b_f32: 16 blocks of D(4 px x 4 cout) += A(4 px
+// x 1) W(1 x 4 cout) per instruction, one tap k = (ci, dy, dx) per instruction in conv_pixel's order from the
+// bias, so each output is the VALU form's fma chain bit for bit (K = 1: one fma per instruction).  Lane l:
+// block b = l >> 2 of the tile, A row / pixel i = l & 3 (a 2 x 2 block: (i >> 1, i & 1)), B / D column
+// c = l & 3 (an output channel of the group), D rows r = the block's 4 pixels (the 2 x 2 MaxPool: a max over
+// the lane's registers).  A tile is 2 x 8 blocks (4 x 16 pixels).  Activations between these layers are
+// NHWC ([y][x][c], unpadded): one ds_read_b128 brings a window position's 4 input channels (L1: 9 reads for
+// a tile's 36 taps, the VALU form 16 exec-masked reads per channel); out-of-image taps are zeroed by select.
+#ifndef GD_SN_MFMA4
+#define GD_SN_MFMA4 0
+#endif
+// in: NHWC [S][S][CIN] -> conv3x3 + bias + ReLU (+ MaxPool2d(2)) -> OUTL 0: NHWC [SO][SO][COUT];
+// OUTL 1: [COUT][SO + 2][RSO] with a zero halo (the MFMA 16-channel stage's input; the halo written elsewhere)
+template <int CIN, int COUT, int S, bool POOL, int OUTL, int RSO = 0>
+__device__ __forceinline__ void conv_mfma4(const float* in, float* out, const float* __restrict__ w,
+                                           const float* __restrict__ b, int tid) {
+    constexpr int K = CIN * 9, NG = COUT / 4, SO = POOL ? S / 2 : S, BPR = S / 2, TPR = BPR / 8;
+    constexpr int NT = (S / 4) * TPR, NW = kThreads / 64;
+    static_assert(COUT % 4 == 0 && CIN % 4 == 0 || CIN == 1, "channel groups of 4");
+    const int wave = tid >> 6, lane = tid & 63, blk = lane >> 2, i = lane & 3, c = lane & 3;
+#pragma unroll 1
+    for (int cg = 0; cg < NG; ++cg) {
+        float bw[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) bw[k] = w[k * COUT + 4 * cg + c];
+        const float bias = b[4 * cg + c];
+#pragma unroll 1
+        for (int t = wave; t < NT; t += NW) {
+            const int tr = t / TPR, tc = t - tr * TPR;
+            const int by = 2 * tr + (blk >> 3), bx = 8 * tc + (blk & 7);
+            const int y = 2 * by + (i >> 1), x = 2 * bx + (i & 1);
+            float av[9][CIN];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const int yy = y + dy - 1, xx = x + dx - 1;
+                    const bool ok = yy >= 0 && yy < S && xx >= 0 && xx < S;
+                    const float* src = in + (ok ? (yy * S + xx) * CIN : 0);
+                    if constexpr (CIN == 1) {
+                        const float v = *src;
+                        av[dy * 3 + dx][0] = ok ? v : 0.f;
+                    } else {
+#pragma unroll
+                        for (int c4 = 0; c4 < CIN; c4 += 4) {
+                            const float4 v = *reinterpret_cast<const float4*>(src + c4);
+                            av[dy * 3 + dx][c4 + 0] = ok ? v.x : 0.f;
+                            av[dy * 3 + dx][c4 + 1] = ok ? v.y : 0.f;
+                            av[dy * 3 + dx][c4 + 2] = ok ? v.z : 0.f;
+                            av[dy * 3 + dx][c4 + 3] = ok ? v.w : 0.f;
+                        }
+                    }
+                }
+            sn_f4 acc = {bias, bias, bias, bias};
+#pragma unroll
+            for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap)
+                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(av[tap][ci], bw[ci * 9 + tap], acc, 0, 0, 0);
+            // lane: block blk's 4 pixels (D rows r: (r >> 1, r & 1)), output channel 4 cg + c
+            const int co = 4 * cg + c;
+            if constexpr (POOL) {
+                const float m = fmaxf(fmaxf(fmaxf(0.f, acc[0]), fmaxf(0.f, acc[1])), fmaxf(fmaxf(0.f, acc[2]), fmaxf(0.f, acc[3])));
+                if constexpr (OUTL == 0) out[(by * SO + bx) * COUT + co] = m;
+                else out[(co * (SO + 2) + by + 1) * RSO + bx + 1] = m;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int yy = 2 * by + (r >> 1), xx = 2 * bx + (r & 1);
+                    const float v = fmaxf(acc[r], 0.f);
+                    if constexpr (OUTL == 0) out[(yy * SO + xx) * COUT + co] = v;
+                    else out[(co * (SO + 2) + yy + 1) * RSO + xx + 1] = v;
+                }
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, int kx) {
     // otf: [65][128] half spectrum (kx-major); |H(ky,kx)|^2 for any kx via Hermitian symmetry
     if (kx > 64) {
@@ -301,6 +379,37 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     __syncthreads();                                                                             \
     SN_TRACE(3 + l);
     constexpr int R16 = kRS16;
+#if GD_SN_MFMA && GD_SN_MFMA4
+    // layers 0-3 on v_mfma_f32_4x4x1_16b_f32, NHWC activations (conv_mfma4), then the 16-channel stage
+    {
+        constexpr int P16 = R16, P8 = kRS8P;
+        conv_mfma4<1, 4, 64, false, 0>(A, B, P + woff(0), P + woff(0) + 4 * 1 * 9, tid);   // B [64][64][4]
+        __syncthreads();
+        SN_TRACE(3);
+        conv_mfma4<4, 4, 64, true, 0>(B, A, P + woff(1), P + woff(1) + 4 * 4 * 9, tid);    // A [32][32][4]
+        __syncthreads();
+        SN_TRACE(4);
+        conv_mfma4<4, 8, 32, false, 0>(A, B, P + woff(2), P + woff(2) + 8 * 4 * 9, tid);   // B [32][32][8]
+        __syncthreads();
+        SN_TRACE(5);
+        zero_halo<8, 16, P16>(A, tid);
+        conv_mfma4<8, 8, 32, true, 1, P16>(B, A, P + woff(3), P + woff(3) + 8 * 8 * 9, tid);  // A [8][18][P16]
+        __syncthreads();
+        SN_TRACE(6);
+        conv_mfma<8, 16, false, P16, P16, 0>(A, B, P + woff(4), P + woff(4) + 16 * 8 * 9, tid);
+        __syncthreads();
+        SN_TRACE(7);
+        conv_mfma<16, 16, true, P16, P8, 0>(B, A, P + woff(5), P + woff(5) + 16 * 16 * 9, tid);
+        __syncthreads();
+        SN_TRACE(8);
+        conv_mfma<16, 8, false, P8, P8, 0>(A, B, P + woff(6), P + woff(6) + 16 * 16 * 9, tid);
+        __syncthreads();
+        SN_TRACE(9);
+        conv_mfma<16, 8, false, P8, P8, 1>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
+        SN_TRACE(10);
+        return;
+    }
+#endif
     GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64, 64, 64)   // B[4][64][64]
     GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64, 64, 32)          // A[4][32][32]   (+ MaxPool of Down(4,8))
     GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64), 32, 32)   // B[8][32][32]
