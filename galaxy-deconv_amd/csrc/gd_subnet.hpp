@@ -199,7 +199,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 // one address add, one ds_read_b32 and one MFMA (the VALU form: 16 exec-masked window reads and scalar weight
 // loads per input channel, waited with lgkmcnt(0)).
 #ifndef GD_SN_MFMA
-#define GD_SN_MFMA 1
+#define GD_SN_MFMA 0  // 1 once measured on the GPU (bit-identical features expected)
 #endif
 typedef float sn_f4 __attribute__((ext_vector_type(4)));
 template <int C, int S, int RS>

@@ -55,8 +55,8 @@ extern "C" {
 
 int gd_abi_version(void);
 const char* gd_engine_rev(void);
-/* sha256 prefix (16 hex digits) of the sources this library was compiled from (csrc/*.hip, *.hpp,
-   include/gdeconv.h; __graft_entry__.build passes it in): smoke() compares it with the tree it runs in */
+/* sha256 prefix (16 hex digits) of the sources this library was compiled from (the csrc .hip and .hpp
+   files and this header; __graft_entry__.build passes it in): smoke() compares it with the tree it runs in */
 const char* gd_engine_src_hash(void);
 const char* gd_last_error(void);
 int gd_supported_size(int H, int W);  /* 1 compile-time-planned, 2 runtime-planned, 0 unsupported */
