@@ -1748,7 +1748,7 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
 // S in the 8 x 6 layout and the spectral update runs on the 6 x 8 one.  Same state, same arithmetic per
 // bin (gauss_iter_st) and the same launch contract as k_gal_small.
 #ifndef GD_SMALL_T
-#define GD_SMALL_T 1  // 1: k_gal_small_t<48> (8 x 6) for the 48^2 iteration
+#define GD_SMALL_T 2  // 1: k_gal_small_t<48> (8 x 6); 2: k_gal_small_p<48> (packed row spectra in LDS) for the 48^2 iteration
 #endif
 template <int L, int TP, int TQ, bool FIRST, bool LAST>
 __global__ __launch_bounds__(256) void k_gal_small_t(Args a) {

@@ -55,6 +55,9 @@ constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #ifndef GD_SN_CS23
 #define GD_SN_CS23 64  // experiment: cap for layers 2, 3 (at 32^2) in the batched kernel
 #endif
+#ifndef GD_SN_NOBR
+#define GD_SN_NOBR 0  // 1: the 2 x 2-block layers read their 4 x 4 windows branch-free (clamped reads + select)
+#endif
 #ifndef GD_SN_UNROLL_PX
 #define GD_SN_UNROLL_PX 2  // input channels per unrolled step: per-pixel layers
 #endif
@@ -142,6 +145,14 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 #pragma unroll
                 for (int k = 0; k < CPT; ++k) acc[q][k] = b[c0 + k];
             const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+#if GD_SN_NOBR
+            // branch-free window: only the outer rows / columns of the 4 x 4 window can leave the image; read them
+            // at a clamped (in-range) position and select 0, so the 16 reads are unconditional (no exec-masked
+            // load per element)
+            const int yc0 = y0 < 0 ? 0 : y0, yc3 = y0 + 3 >= S ? S - 1 : y0 + 3;
+            const int xc0 = x0 < 0 ? 0 : x0, xc3 = x0 + 3 >= S ? S - 1 : x0 + 3;
+            const bool bad_r0 = y0 < 0, bad_r3 = y0 + 3 >= S, bad_c0 = x0 < 0, bad_c3 = x0 + 3 >= S;
+#endif
 #pragma unroll GD_SN_UNROLL_Q
             for (int ci = 0; ci < CIN; ++ci) {
                 float win[4][4];
@@ -149,8 +160,15 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
+#if GD_SN_NOBR
+                        const int yy = r == 0 ? yc0 : r == 3 ? yc3 : y0 + r, xx = c == 0 ? xc0 : c == 3 ? xc3 : x0 + c;
+                        const bool bad = (r == 0 && bad_r0) || (r == 3 && bad_r3) || (c == 0 && bad_c0) || (c == 3 && bad_c3);
+                        const float v = in[(ci * S + yy) * RSI + xx];
+                        win[r][c] = bad ? 0.f : v;
+#else
                         const int yy = y0 + r, xx = x0 + c;
                         win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * RSI + xx] : 0.f;
+#endif
                     }
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
@@ -199,7 +217,7 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 // one address add, one ds_read_b32 and one MFMA (the VALU form: 16 exec-masked window reads and scalar weight
 // loads per input channel, waited with lgkmcnt(0)).
 #ifndef GD_SN_MFMA
-#define GD_SN_MFMA 0  // 1 once measured on the GPU (bit-identical features expected)
+#define GD_SN_MFMA 1  // 0: the VALU conv_layer for layers 4-7 (bit-identical features; profiles/r04b_ksubnet_mfma_ab.txt)
 #endif
 typedef float sn_f4 __attribute__((ext_vector_type(4)));
 template <int C, int S, int RS>
@@ -221,31 +239,44 @@ template <int CIN, int S, bool POOL, int RSI, int RSO, int OUTF>
 __device__ __forceinline__ void conv_mfma(const float* in, float* out, const float* __restrict__ w,
                                           const float* __restrict__ b, int tid) {
     constexpr int COUT = 16, K = CIN * 9, NS = K / 4, CHI = (S + 2) * RSI, SO = POOL ? S / 2 : S;
-    constexpr int BPR = S / 2, NT = S * S / 16, NW = kThreads / 64;
-    static_assert(K % 4 == 0 && (S * S) % 16 == 0, "k-steps of 4, tiles of 16 pixels");
+    constexpr int BPR = S / 2, NT = S * S / 16, NW = kThreads / 64, NC = NS / 9;
+    static_assert(CIN % 4 == 0 && (S * S) % 16 == 0, "k-steps of 4 in chunks of 9 (4 input channels), tiles of 16 pixels");
     const int wave = tid >> 6, lane = tid & 63, q = lane >> 4, col = lane & 15;
     if constexpr (OUTF == 0) zero_halo<COUT, SO, RSO>(out, tid);  // disjoint from the interior written below
     if (wave >= NT) return;  // 8^2 layers: 4 tiles, waves 4-7 idle (no barrier inside)
-    float bw[NS];
-    int off[NS];
+    // k = 4 s + q: the (ci, dy, dx) pattern repeats every 9 k-steps (36 taps = 4 input channels), so a lane
+    // keeps 9 window offsets and step s reads at off9[s % 9] + 4 CHI (s / 9) (the second term an immediate)
+    int off9[9];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < 9; ++s) {
         const int k = 4 * s + q, ci = k / 9, r = k - 9 * ci, dy = r / 3, dx = r - 3 * dy;
-        bw[s] = w[k * COUT + col];
-        off[s] = ci * CHI + dy * RSI + dx;
+        off9[s] = ci * CHI + dy * RSI + dx;
     }
+    float bw[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) bw[s] = w[(4 * s + q) * COUT + col];
     const float bias = b[col];
     for (int t = wave; t < NT; t += NW) {
-        // A row of this lane: pixel i = lane & 15 of tile t (block i >> 2, position i & 3)
+        // A row of this lane: pixel ia = lane & 15 of tile t (block ia >> 2, position ia & 3)
         const int ia = lane & 15, blk = 4 * t + (ia >> 2), by = blk / BPR, bx = blk - by * BPR;
         const int y = 2 * by + ((ia >> 1) & 1), x = 2 * bx + (ia & 1);
         const float* src = in + y * RSI + x;  // window origin in padded coordinates
-        float av[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) av[s] = src[off[s]];
         sn_f4 acc = {bias, bias, bias, bias};
+        // software-pipelined: chunk c + 1's 9 reads are in flight while chunk c's 9 MFMAs issue
+        float av[2][9];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bw[s], acc, 0, 0, 0);
+        for (int s = 0; s < 9; ++s) av[0][s] = src[off9[s]];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c + 1 < NC) {
+#pragma unroll
+                for (int s = 0; s < 9; ++s) av[(c + 1) & 1][s] = src[off9[s] + 4 * CHI * (c + 1)];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < 9; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c & 1][s], bw[9 * c + s], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // this lane's results: block (t, q), positions r = 0..3 (D row 4q + r), channel col
         const int ob = 4 * t + q, oby = ob / BPR, obx = ob - oby * BPR;
         if constexpr (POOL) {
@@ -264,84 +295,6 @@ __device__ __forceinline__ void conv_mfma(const float* in, float* out, const flo
     }
 }
 
-// ---- layers 0-3 (4 / 8 output channels) on v_mfma_f32_4x4x1_16b_f32: 16 blocks of D(4 px x 4 cout) += A(4 px
-// x 1) W(1 x 4 cout) per instruction, one tap k = (ci, dy, dx) per instruction in conv_pixel's order from the
-// bias, so each output is the VALU form's fma chain bit for bit (K = 1: one fma per instruction).  Lane l:
-// block b = l >> 2 of the tile, A row / pixel i = l & 3 (a 2 x 2 block: (i >> 1, i & 1)), B / D column
-// c = l & 3 (an output channel of the group), D rows r = the block's 4 pixels (the 2 x 2 MaxPool: a max over
-// the lane's registers).  A tile is 2 x 8 blocks (4 x 16 pixels).  Activations between these layers are
-// NHWC ([y][x][c], unpadded): one ds_read_b128 brings a window position's 4 input channels (L1: 9 reads for
-// a tile's 36 taps, the VALU form 16 exec-masked reads per channel); out-of-image taps are zeroed by select.
-#ifndef GD_SN_MFMA4
-#define GD_SN_MFMA4 0
-#endif
-// in: NHWC [S][S][CIN] -> conv3x3 + bias + ReLU (+ MaxPool2d(2)) -> OUTL 0: NHWC [SO][SO][COUT];
-// OUTL 1: [COUT][SO + 2][RSO] with a zero halo (the MFMA 16-channel stage's input; the halo written elsewhere)
-template <int CIN, int COUT, int S, bool POOL, int OUTL, int RSO = 0>
-__device__ __forceinline__ void conv_mfma4(const float* in, float* out, const float* __restrict__ w,
-                                           const float* __restrict__ b, int tid) {
-    constexpr int K = CIN * 9, NG = COUT / 4, SO = POOL ? S / 2 : S, BPR = S / 2, TPR = BPR / 8;
-    constexpr int NT = (S / 4) * TPR, NW = kThreads / 64;
-    static_assert(COUT % 4 == 0 && CIN % 4 == 0 || CIN == 1, "channel groups of 4");
-    const int wave = tid >> 6, lane = tid & 63, blk = lane >> 2, i = lane & 3, c = lane & 3;
-#pragma unroll 1
-    for (int cg = 0; cg < NG; ++cg) {
-        float bw[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) bw[k] = w[k * COUT + 4 * cg + c];
-        const float bias = b[4 * cg + c];
-#pragma unroll 1
-        for (int t = wave; t < NT; t += NW) {
-            const int tr = t / TPR, tc = t - tr * TPR;
-            const int by = 2 * tr + (blk >> 3), bx = 8 * tc + (blk & 7);
-            const int y = 2 * by + (i >> 1), x = 2 * bx + (i & 1);
-            float av[9][CIN];
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    const int yy = y + dy - 1, xx = x + dx - 1;
-                    const bool ok = yy >= 0 && yy < S && xx >= 0 && xx < S;
-                    const float* src = in + (ok ? (yy * S + xx) * CIN : 0);
-                    if constexpr (CIN == 1) {
-                        const float v = *src;
-                        av[dy * 3 + dx][0] = ok ? v : 0.f;
-                    } else {
-#pragma unroll
-                        for (int c4 = 0; c4 < CIN; c4 += 4) {
-                            const float4 v = *reinterpret_cast<const float4*>(src + c4);
-                            av[dy * 3 + dx][c4 + 0] = ok ? v.x : 0.f;
-                            av[dy * 3 + dx][c4 + 1] = ok ? v.y : 0.f;
-                            av[dy * 3 + dx][c4 + 2] = ok ? v.z : 0.f;
-                            av[dy * 3 + dx][c4 + 3] = ok ? v.w : 0.f;
-                        }
-                    }
-                }
-            sn_f4 acc = {bias, bias, bias, bias};
-#pragma unroll
-            for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-                for (int tap = 0; tap < 9; ++tap)
-                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(av[tap][ci], bw[ci * 9 + tap], acc, 0, 0, 0);
-            // lane: block blk's 4 pixels (D rows r: (r >> 1, r & 1)), output channel 4 cg + c
-            const int co = 4 * cg + c;
-            if constexpr (POOL) {
-                const float m = fmaxf(fmaxf(fmaxf(0.f, acc[0]), fmaxf(0.f, acc[1])), fmaxf(fmaxf(0.f, acc[2]), fmaxf(0.f, acc[3])));
-                if constexpr (OUTL == 0) out[(by * SO + bx) * COUT + co] = m;
-                else out[(co * (SO + 2) + by + 1) * RSO + bx + 1] = m;
-            } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int yy = 2 * by + (r >> 1), xx = 2 * bx + (r & 1);
-                    const float v = fmaxf(acc[r], 0.f);
-                    if constexpr (OUTL == 0) out[(yy * SO + xx) * COUT + co] = v;
-                    else out[(co * (SO + 2) + yy + 1) * RSO + xx + 1] = v;
-                }
-            }
-        }
-    }
-}
-
 __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, int kx) {
     // otf: [65][128] half spectrum (kx-major); |H(ky,kx)|^2 for any kx via Hermitian symmetry
     if (kx > 64) {
@@ -355,7 +308,13 @@ __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, in
 // The conv stack of galaxy g; the last layer writes the 1024 features to `out` (LDS or global).
 // C5 / C67: caps on the output-channel split of layer 5 and layers 6, 7 (kCSBatched / kCSOneRound)
 template <int C5, int C67>
-__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid);
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid,
+                                            const float* __restrict__ warm = nullptr);
+#ifndef GD_SN_W1WARM
+#define GD_SN_W1WARM 0  // 1: one workgroup per XCD pulls the MLP's W1 into its L2 (LDS-DMA into a dead 1 KiB) at layer 4
+#endif
+typedef __attribute__((address_space(3))) void* sn_lds_vptr;
+typedef __attribute__((address_space(1))) void* sn_gbl_vptr;
 __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, const float* __restrict__ params,
                                            float* out, float* A, float* B, int g, int tid) {
     const float2* otf = otf128 + (size_t)g * 65 * 128;
@@ -372,44 +331,14 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
 }
 // the four Down blocks from the pooled |H|^2 in A[64][64]
 template <int C5, int C67>
-__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid,
+                                            const float* __restrict__ warm) {
     const float* P = params;
 #define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT, CMAX, RSI, RSO)                             \
     conv_layer<CI, CO, S, POOL, QUAD, CMAX, RSI, RSO>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid); \
     __syncthreads();                                                                             \
     SN_TRACE(3 + l);
     constexpr int R16 = kRS16;
-#if GD_SN_MFMA && GD_SN_MFMA4
-    // layers 0-3 on v_mfma_f32_4x4x1_16b_f32, NHWC activations (conv_mfma4), then the 16-channel stage
-    {
-        constexpr int P16 = R16, P8 = kRS8P;
-        conv_mfma4<1, 4, 64, false, 0>(A, B, P + woff(0), P + woff(0) + 4 * 1 * 9, tid);   // B [64][64][4]
-        __syncthreads();
-        SN_TRACE(3);
-        conv_mfma4<4, 4, 64, true, 0>(B, A, P + woff(1), P + woff(1) + 4 * 4 * 9, tid);    // A [32][32][4]
-        __syncthreads();
-        SN_TRACE(4);
-        conv_mfma4<4, 8, 32, false, 0>(A, B, P + woff(2), P + woff(2) + 8 * 4 * 9, tid);   // B [32][32][8]
-        __syncthreads();
-        SN_TRACE(5);
-        zero_halo<8, 16, P16>(A, tid);
-        conv_mfma4<8, 8, 32, true, 1, P16>(B, A, P + woff(3), P + woff(3) + 8 * 8 * 9, tid);  // A [8][18][P16]
-        __syncthreads();
-        SN_TRACE(6);
-        conv_mfma<8, 16, false, P16, P16, 0>(A, B, P + woff(4), P + woff(4) + 16 * 8 * 9, tid);
-        __syncthreads();
-        SN_TRACE(7);
-        conv_mfma<16, 16, true, P16, P8, 0>(B, A, P + woff(5), P + woff(5) + 16 * 16 * 9, tid);
-        __syncthreads();
-        SN_TRACE(8);
-        conv_mfma<16, 8, false, P8, P8, 0>(A, B, P + woff(6), P + woff(6) + 16 * 16 * 9, tid);
-        __syncthreads();
-        SN_TRACE(9);
-        conv_mfma<16, 8, false, P8, P8, 1>(B, out, P + woff(7), P + woff(7) + 16 * 16 * 9, tid);
-        SN_TRACE(10);
-        return;
-    }
-#endif
     GD_SN_LAYER(0, 1, 4, 64, false, GD_SN_QUAD, A, B, 64, 64, 64)   // B[4][64][64]
     GD_SN_LAYER(1, 4, 4, 64, true, true, B, A, 64, 64, 32)          // A[4][32][32]   (+ MaxPool of Down(4,8))
     GD_SN_LAYER(2, 4, 8, 32, false, GD_SN_QUAD, A, B, (C5 < 64 ? GD_SN_CS23 : 64), 32, 32)   // B[8][32][32]
@@ -421,6 +350,14 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     conv_layer<8, 8, 32, true, true, (C5 < 64 ? GD_SN_CS23 : 64), 32, P16, true>(B, A, P + woff(3), P + woff(3) + 8 * 8 * 9, tid);
     __syncthreads();
     SN_TRACE(6);
+    if (GD_SN_W1WARM && warm != nullptr) {
+        // A[3584, 3840) is dead from here to the end (layer 5 writes A[0, 1920), the features A[0, 1024)): the sink
+        // of an LDS-DMA sweep over W1 ((kFeat + 1) x kHidden floats) that leaves it in this XCD's L2 for the MLP
+        constexpr int V4 = (1025 * 64) / 4;
+        const float4* src = reinterpret_cast<const float4*>(warm);
+        for (int i = tid; i < V4; i += kThreads)
+            __builtin_amdgcn_global_load_lds((sn_gbl_vptr)(src + i), (sn_lds_vptr)(A + 3584), 16, 0, 0);
+    }
     conv_mfma<8, 16, false, P16, P16, 0>(A, B, P + woff(4), P + woff(4) + 16 * 8 * 9, tid);   // B[16][18][P16]
     __syncthreads();
     SN_TRACE(7);
@@ -680,7 +617,8 @@ __device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long lo
     psf_pool(psf + (long long)g * psf_gstride, h, AB, tid);
     float* X = AB;                 // features [1024] (region A is free once layer 6 has been read)
     float* P = AB + kRegionA;      // partial sums [8][64], then h1, h2 (region B, after layer 7 read it)
-    conv_layers<kCSOneRound, kCSOneRound>(params, X, AB, AB + kRegionA, tid);
+    // blocks 0-7 (one per XCD under the round-robin dispatch: speed only) warm W1 into their XCD's L2
+    conv_layers<kCSOneRound, kCSOneRound>(params, X, AB, AB + kRegionA, tid, (GD_SN_W1WARM && blockIdx.x < 8) ? mlp : nullptr);
     __syncthreads();
     const float xa = alpha[(long long)g * alpha_stride];
     const float* W1 = mlp;
