@@ -3282,6 +3282,20 @@ int gd_set_fused_iteration(int on) {
     return old;
 }
 
+// the batched SubNet MLP over N feature vectors (MFMA chains, or k_subnet_mlp: bit-identical rhos)
+static int subnet_mlp(const float* feat, const float* mlp_params, const float* alpha, long long alpha_stride, float* rhos,
+                      int n_out, int N, hipStream_t stream) {
+    ProfScope ps("k_subnet_mlp<128,0>", stream, 1);
+    if (GD_MLP_MFMA) {
+        hipLaunchKernelGGL(gd::subnet::k_subnet_mlp_mfma, dim3((N + gd::subnet::kMG - 1) / gd::subnet::kMG),
+                           dim3(gd::subnet::kMlpThreads), 0, stream, feat, mlp_params, alpha, alpha_stride, rhos, n_out, N);
+        return check_launch("k_subnet_mlp_mfma");
+    }
+    hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((N + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
+                       dim3(gd::subnet::kMlpThreads), 0, stream, feat, mlp_params, alpha, alpha_stride, rhos, n_out, N);
+    return check_launch("k_subnet_mlp");
+}
+
 int gd_subnet_param_count(void) { return gd::subnet::kParams; }
 
 int gd_subnet_mlp_param_count(int n_out) {
@@ -3294,11 +3308,7 @@ int gd_subnet_rhos(const void* otf128_half, const float* params, const float* ml
     if (n_out < 1 || n_out > gd::subnet::kMaxOut) return fail(GD_ERR_ARG, "n_out must be in [1, 64]");
     if (N == 0) return GD_OK;
     GD_TRY(gd_subnet_features(otf128_half, params, feat, N, stream));
-    ProfScope ps("k_subnet_mlp<128,0>", (hipStream_t)stream, 1);
-    hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((N + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
-                       dim3(gd::subnet::kMlpThreads), 0, (hipStream_t)stream, feat, mlp_params, alpha, alpha_stride,
-                       rhos, n_out, N);
-    return check_launch("k_subnet_mlp");
+    return subnet_mlp(feat, mlp_params, alpha, alpha_stride, rhos, n_out, N, (hipStream_t)stream);
 }
 
 int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const float* params, const float* mlp_params,
@@ -3320,11 +3330,7 @@ int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const flo
                            (hipStream_t)stream, psf, psf_gstride, h, params, feat, N);
         GD_TRY(check_launch("k_subnet_features_psf"));
     }
-    ProfScope ps("k_subnet_mlp<128,0>", (hipStream_t)stream, 1);
-    hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((N + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
-                       dim3(gd::subnet::kMlpThreads), 0, (hipStream_t)stream, feat, mlp_params, alpha, alpha_stride,
-                       rhos, n_out, N);
-    return check_launch("k_subnet_mlp");
+    return subnet_mlp(feat, mlp_params, alpha, alpha_stride, rhos, n_out, N, (hipStream_t)stream);
 }
 
 int gd_admm_init_subnet_supported(int N, int H, int W, int h, int w, int llh, int n_out) {

@@ -55,9 +55,6 @@ constexpr int kCSBatched = GD_SN_CS_BATCHED, kCSOneRound = 64;
 #ifndef GD_SN_CS23
 #define GD_SN_CS23 64  // experiment: cap for layers 2, 3 (at 32^2) in the batched kernel
 #endif
-#ifndef GD_SN_NOBR
-#define GD_SN_NOBR 0  // 1: the 2 x 2-block layers read their 4 x 4 windows branch-free (clamped reads + select)
-#endif
 #ifndef GD_SN_UNROLL_PX
 #define GD_SN_UNROLL_PX 2  // input channels per unrolled step: per-pixel layers
 #endif
@@ -145,14 +142,6 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
 #pragma unroll
                 for (int k = 0; k < CPT; ++k) acc[q][k] = b[c0 + k];
             const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
-#if GD_SN_NOBR
-            // branch-free window: only the outer rows / columns of the 4 x 4 window can leave the image; read them
-            // at a clamped (in-range) position and select 0, so the 16 reads are unconditional (no exec-masked
-            // load per element)
-            const int yc0 = y0 < 0 ? 0 : y0, yc3 = y0 + 3 >= S ? S - 1 : y0 + 3;
-            const int xc0 = x0 < 0 ? 0 : x0, xc3 = x0 + 3 >= S ? S - 1 : x0 + 3;
-            const bool bad_r0 = y0 < 0, bad_r3 = y0 + 3 >= S, bad_c0 = x0 < 0, bad_c3 = x0 + 3 >= S;
-#endif
 #pragma unroll GD_SN_UNROLL_Q
             for (int ci = 0; ci < CIN; ++ci) {
                 float win[4][4];
@@ -160,15 +149,8 @@ __device__ __forceinline__ void conv_layer(const float* in, float* out, const fl
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-#if GD_SN_NOBR
-                        const int yy = r == 0 ? yc0 : r == 3 ? yc3 : y0 + r, xx = c == 0 ? xc0 : c == 3 ? xc3 : x0 + c;
-                        const bool bad = (r == 0 && bad_r0) || (r == 3 && bad_r3) || (c == 0 && bad_c0) || (c == 3 && bad_c3);
-                        const float v = in[(ci * S + yy) * RSI + xx];
-                        win[r][c] = bad ? 0.f : v;
-#else
                         const int yy = y0 + r, xx = x0 + c;
                         win[r][c] = (yy >= 0 && yy < S && xx >= 0 && xx < S) ? in[(ci * S + yy) * RSI + xx] : 0.f;
-#endif
                     }
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
@@ -308,13 +290,7 @@ __device__ __forceinline__ float mag2(const float2* __restrict__ otf, int ky, in
 // The conv stack of galaxy g; the last layer writes the 1024 features to `out` (LDS or global).
 // C5 / C67: caps on the output-channel split of layer 5 and layers 6, 7 (kCSBatched / kCSOneRound)
 template <int C5, int C67>
-__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid,
-                                            const float* __restrict__ warm = nullptr);
-#ifndef GD_SN_W1WARM
-#define GD_SN_W1WARM 0  // 1: one workgroup per XCD pulls the MLP's W1 into its L2 (LDS-DMA into a dead 1 KiB) at layer 4
-#endif
-typedef __attribute__((address_space(3))) void* sn_lds_vptr;
-typedef __attribute__((address_space(1))) void* sn_gbl_vptr;
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid);
 __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, const float* __restrict__ params,
                                            float* out, float* A, float* B, int g, int tid) {
     const float2* otf = otf128 + (size_t)g * 65 * 128;
@@ -331,8 +307,7 @@ __device__ __forceinline__ void conv_stack(const float2* __restrict__ otf128, co
 }
 // the four Down blocks from the pooled |H|^2 in A[64][64]
 template <int C5, int C67>
-__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid,
-                                            const float* __restrict__ warm) {
+__device__ __forceinline__ void conv_layers(const float* __restrict__ params, float* out, float* A, float* B, int tid) {
     const float* P = params;
 #define GD_SN_LAYER(l, CI, CO, S, POOL, QUAD, IN, OUT, CMAX, RSI, RSO)                             \
     conv_layer<CI, CO, S, POOL, QUAD, CMAX, RSI, RSO>(IN, OUT, P + woff(l), P + woff(l) + CO * CI * 9, tid); \
@@ -350,14 +325,6 @@ __device__ __forceinline__ void conv_layers(const float* __restrict__ params, fl
     conv_layer<8, 8, 32, true, true, (C5 < 64 ? GD_SN_CS23 : 64), 32, P16, true>(B, A, P + woff(3), P + woff(3) + 8 * 8 * 9, tid);
     __syncthreads();
     SN_TRACE(6);
-    if (GD_SN_W1WARM && warm != nullptr) {
-        // A[3584, 3840) is dead from here to the end (layer 5 writes A[0, 1920), the features A[0, 1024)): the sink
-        // of an LDS-DMA sweep over W1 ((kFeat + 1) x kHidden floats) that leaves it in this XCD's L2 for the MLP
-        constexpr int V4 = (1025 * 64) / 4;
-        const float4* src = reinterpret_cast<const float4*>(warm);
-        for (int i = tid; i < V4; i += kThreads)
-            __builtin_amdgcn_global_load_lds((sn_gbl_vptr)(src + i), (sn_lds_vptr)(A + 3584), 16, 0, 0);
-    }
     conv_mfma<8, 16, false, P16, P16, 0>(A, B, P + woff(4), P + woff(4) + 16 * 8 * 9, tid);   // B[16][18][P16]
     __syncthreads();
     SN_TRACE(7);
@@ -601,6 +568,129 @@ __global__ __launch_bounds__(kMlpThreads) void k_subnet_mlp(const float* __restr
     }
 }
 
+// ---- the batched MLP on the matrix cores (GD_MLP_MFMA): k_subnet_mlp's arithmetic as v_mfma_f32_16x16x4_f32
+// chains, 16 galaxies (M) x 16 outputs (N) per tile.  Every sum keeps its order: layer 1's partial of wave w
+// is the k-ordered chain over inputs [128 w, 128 w + 128) from 0 (wave 7 then adds the alpha input as one more
+// k-step whose other three slots are 0 * 0), the 8 partials are added in wave order, layers 2 and 3 are chains
+// over their 64 inputs from 0 - the f32 MFMA is a k-ordered fmaf chain, so the rhos are bit-identical to
+// k_subnet_mlp's and to the one-launch k_subnet_rhos_psf's.  W1 is read once per 16 galaxies (k_subnet_mlp:
+// per 8) and a wave's 4 N-tiles share each A read; 1/16 of k_subnet_mlp's instructions per product.
+#ifndef GD_MLP_MFMA
+#define GD_MLP_MFMA 1
+#endif
+constexpr int kMG = 16, kXLD = 1026;  // galaxies per workgroup; X row stride (2 mod 32: conflict-free A reads)
+__global__ __launch_bounds__(kMlpThreads) void k_subnet_mlp_mfma(const float* __restrict__ feat,
+                                                                const float* __restrict__ mlp,
+                                                                const float* __restrict__ alpha, long long alpha_stride,
+                                                                float* __restrict__ rhos, int n_out, int N) {
+    static_assert(kMlpThreads == 512 && kHidden == 64 && kFeat == 1024, "8 waves x 128 inputs; 4 N-tiles of 16");
+    __shared__ __attribute__((aligned(16))) float X[kMG * kXLD];  // [galaxy][input], then the layer-1 partials
+    __shared__ float Hs[2][kMG][kHidden];
+    const int tid = threadIdx.x, g0 = blockIdx.x * kMG;
+    const int ng = N - g0 < kMG ? N - g0 : kMG;
+    for (int i = tid; i < kMG * (kFeat / 2); i += kMlpThreads) {
+        const int gg = i / (kFeat / 2), f2 = i - gg * (kFeat / 2);
+        const float2 v = gg < ng ? reinterpret_cast<const float2*>(feat + (size_t)(g0 + gg) * kFeat)[f2] : make_float2(0.f, 0.f);
+        *reinterpret_cast<float2*>(X + gg * kXLD + 2 * f2) = v;
+    }
+    if (tid < kMG) {
+        X[tid * kXLD + kFeat] = tid < ng ? alpha[(long long)(g0 + tid) * alpha_stride] : 0.f;
+        X[tid * kXLD + kFeat + 1] = 0.f;
+    }
+    __syncthreads();
+    const float* W1 = mlp;
+    const float* b1 = W1 + (kFeat + 1) * kHidden;
+    const float* W2 = b1 + kHidden;
+    const float* b2 = W2 + kHidden * kHidden;
+    const float* W3 = b2 + kHidden;
+    const float* b3 = W3 + kHidden * n_out;
+    const int w = tid >> 6, lane = tid & 63, gi = lane & 15, qk = lane >> 4, col = lane & 15;
+    // layer 1: wave w, inputs [128 w, 128 w + 128), all 64 outputs (4 N-tiles), chains from 0
+    sn_f4 acc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[nt] = sn_f4{0.f, 0.f, 0.f, 0.f};
+    {
+        constexpr int CH = 8, NCH = (kFeat / kMlpWaves) / 4 / CH;  // 32 k-steps per wave in chunks of 8
+        const float* xa = X + gi * kXLD + 128 * w + qk;
+        const float* wb = W1 + (size_t)(128 * w + qk) * kHidden + col;
+        float bv[2][CH][4];
+#pragma unroll
+        for (int s = 0; s < CH; ++s)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) bv[0][s][nt] = wb[(4 * s) * kHidden + 16 * nt];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c + 1 < NCH) {
+#pragma unroll
+                for (int s = 0; s < CH; ++s)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) bv[(c + 1) & 1][s][nt] = wb[(4 * (CH * (c + 1) + s)) * kHidden + 16 * nt];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const float a = xa[4 * (CH * c + s)];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[c & 1][s][nt], acc[nt], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (w == kMlpWaves - 1) {  // the alpha input (k = 1024) as one k-step, the other slots 0 * 0
+            const float a = qk == 0 ? X[gi * kXLD + kFeat] : 0.f;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float bb = qk == 0 ? W1[kFeat * kHidden + 16 * nt + col] : 0.f;
+                acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc[nt], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // X read -> the partials P[w][g][o] reuse it
+    float* P = X;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[(w * kMG + 4 * qk + r) * kHidden + 16 * nt + col] = acc[nt][r];
+    __syncthreads();
+    for (int e = tid; e < kMG * kHidden; e += kMlpThreads) {
+        const int gg = e / kHidden, o = e - gg * kHidden;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kMlpWaves; ++ww) v += P[(ww * kMG + gg) * kHidden + o];
+        Hs[0][gg][o] = fmaxf(v + b1[o], 0.f);
+    }
+    __syncthreads();
+    // layer 2: wave w < 4 computes N-tile w, a chain over the 64 inputs from 0
+    if (w < 4) {
+        sn_f4 a2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < kHidden / 4; ++s)
+            a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(Hs[0][gi][4 * s + qk], W2[(4 * s + qk) * kHidden + 16 * w + col], a2, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Hs[1][4 * qk + r][16 * w + col] = fmaxf(a2[r] + b2[16 * w + col], 0.f);
+    }
+    __syncthreads();
+    // layer 3: n_out outputs in N-tiles of 16
+    if (16 * w < n_out) {
+        const int o = 16 * w + col;
+        sn_f4 a3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < kHidden / 4; ++s)
+            a3 = __builtin_amdgcn_mfma_f32_16x16x4f32(Hs[1][gi][4 * s + qk], o < n_out ? W3[(4 * s + qk) * n_out + o] : 0.f,
+                                                      a3, 0, 0, 0);
+        if (o < n_out) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gg = 4 * qk + r;
+                if (gg < ng) {
+                    const float v = a3[r] + b3[o];
+                    // nn.Softplus(beta = 1, threshold = 20), then + 1e-6 (:86)
+                    rhos[(size_t)(g0 + gg) * n_out + o] = (v > 20.f ? v : log1pf(expf(v))) + 1e-6f;
+                }
+            }
+        }
+    }
+}
+
 // ---- the whole SubNet of one galaxy in one workgroup (small batches): k_subnet_features_psf, then the MLP
 // on the workgroup's own feature vector (in LDS), in k_subnet_mlp's summation order (wave q sums inputs
 // [q KQ, (q + 1) KQ) in order, the 8 partial sums added in wave order, layers 2 and 3 in input order), so
@@ -617,8 +707,7 @@ __device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long lo
     psf_pool(psf + (long long)g * psf_gstride, h, AB, tid);
     float* X = AB;                 // features [1024] (region A is free once layer 6 has been read)
     float* P = AB + kRegionA;      // partial sums [8][64], then h1, h2 (region B, after layer 7 read it)
-    // blocks 0-7 (one per XCD under the round-robin dispatch: speed only) warm W1 into their XCD's L2
-    conv_layers<kCSOneRound, kCSOneRound>(params, X, AB, AB + kRegionA, tid, (GD_SN_W1WARM && blockIdx.x < 8) ? mlp : nullptr);
+    conv_layers<kCSOneRound, kCSOneRound>(params, X, AB, AB + kRegionA, tid);
     __syncthreads();
     const float xa = alpha[(long long)g * alpha_stride];
     const float* W1 = mlp;

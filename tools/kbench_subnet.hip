@@ -103,6 +103,29 @@ int main(int argc, char** argv) {
 #endif
     };
     timeit(feats, N, "k_subnet_features_psf");
+    // the batched MLP on those features: k_subnet_mlp (VALU) and k_subnet_mlp_mfma, both into rhosb
+    float* rhosb;
+    CK(hipMalloc(&rhosb, (size_t)NM * n_out * 4));
+    auto mlp_valu = [&](int n) {
+        hipLaunchKernelGGL(gd::subnet::k_subnet_mlp, dim3((n + gd::subnet::kMlpG - 1) / gd::subnet::kMlpG),
+                           dim3(gd::subnet::kMlpThreads), 0, 0, feat, mlp, alpha, 1LL, rhosb, n_out, n);
+    };
+    auto mlp_mfma = [&](int n) {
+        hipLaunchKernelGGL(gd::subnet::k_subnet_mlp_mfma, dim3((n + gd::subnet::kMG - 1) / gd::subnet::kMG),
+                           dim3(gd::subnet::kMlpThreads), 0, 0, feat, mlp, alpha, 1LL, rhosb, n_out, n);
+    };
+    auto rfnv = [&](int n) {
+        std::vector<float> v((size_t)n * n_out);
+        CK(hipMemcpy(v.data(), rhosb, v.size() * 4, hipMemcpyDeviceToHost));
+        unsigned long long h = 1469598103934665603ull;
+        for (float f : v) { unsigned u; memcpy(&u, &f, 4); h = (h ^ u) * 1099511628211ull; }
+        return h;
+    };
+    timeit(mlp_valu, N, "k_subnet_mlp");
+    const unsigned long long h_valu = rfnv(N), h_valu_r = rfnv(Nr);
+    timeit(mlp_mfma, N, "k_subnet_mlp_mfma");
+    printf("batched rhos fnv: k_subnet_mlp %016llx  k_subnet_mlp_mfma %016llx  (first %d: %016llx / %016llx)\n", h_valu,
+           rfnv(N), Nr, h_valu_r, rfnv(Nr));
     timeit(fused, Nr, "k_subnet_rhos_psf");
     std::vector<float> hr(n_out);
     CK(hipMemcpy(hr.data(), rhos, n_out * 4, hipMemcpyDeviceToHost));
