@@ -358,7 +358,9 @@ def main():
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
     generic = args.size not in (32, 48, 64, 96, 128, 256)  # gd_supported_size == 2: gd_generic.hpp
-    use_fused = bool(fused) and not generic and args.llh == "Gaussian"
+    # 160^2 (runtime-planned size) runs its Gaussian iterations fused too (k_gal_mid, gd_engine.hip)
+    mid_fused = bool(fused) and args.size == 160 and args.llh == "Gaussian"
+    use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian"
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
@@ -595,6 +597,8 @@ def main():
                    "ranks_seen": world, "backend": backend or "none",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
+                                               "k_gal_mid (160^2: half spectrum in LDS, 512 threads per galaxy)"
+                                               if mid_fused else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
                                  if use_fused else (rl_impl if rl else
                                                     ("two whole-galaxy passes: k_gal_reg<POIS> (X update, u1, zin) + "

@@ -1965,6 +1965,100 @@ __global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
     GD_TRACE(4);
 }
 
+// ---------------------------------------------------------------- fused Gaussian iteration at 160^2
+// k_gal_small_p's one-pass design for a runtime-planned size whose half spectrum still fits in LDS: at 160^2 the
+// packed row spectra PR[kx][p] take 160 x 81 complex = 101 KiB, the 32 lines' exchange areas 44 KiB, so one
+// 512-thread workgroup per galaxy runs rows -> columns + update -> inverse rows on chip (the runtime-planned
+// three-kernel chain moves ~19 words per pixel through the workspace; this moves 2 img + 5.5 half = 7.5).  Lines
+// are 16 lanes x 10 points (tline_fft<160, 16, 10>: DFT-10 = 2 x 5, then DFT-16 across the lanes; the inverse
+// back), looped over the 80 row pairs / 81 columns.  The state layout is the generic path's [N][K][L] (what
+// its init writes), the per-bin arithmetic gauss_iter_elem's, so this is a drop-in for the C_G_ITER* chain.
+#ifndef GD_MID_FUSED
+#define GD_MID_FUSED 1  // 1: 160^2 Gaussian iterations in one launch (k_gal_mid); 0: the runtime-planned chain
+#endif
+template <int L, int TP, int TQ, int NT, bool FIRST, bool LAST>
+__global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
+    constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1;
+    constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    static_assert(TP * TQ == L && TP >= TQ && TP % 2 == 0 && NT % G == 0, "lines of TP lanes, rows paired per lane");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 PR[L * SP];
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, NT);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
+    __syncthreads();
+    const float* z = a.a0 + (size_t)g * L * L;
+    float2 v[G];
+
+    // R: row pair p -> FFT -> packed spectrum PR[kx][p] (lane j < TQ holds kx = j + TQ k1)
+    for (int p = line; p < L / 2; p += LINES) {
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * p) * L + j + TP * s], z[(2 * p + 1) * L + j + TP * s]);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[(j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();  // all of z read (zin may alias z), PR complete
+
+    // C: column kx (lane j: rows r = j + TP r', separated from the packed columns kx and L - kx), FFT, update,
+    // IFFT, then the next row phase's packed input for both columns written in place (k_gal_small_p's scheme)
+    const bool odd = j & 1;
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[kx * SP + p], Dm = PR[km * SP + p];
+            v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        const bool cl = j < TQ;
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1)
+            v[k1] = gauss_iter_elem<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], r1, r2, r2n, cl, inv_n);
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        const bool self = (kx == 0) || (2 * kx == L);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const float ox = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].x), 0xB1, 0xF, 0xF, false));
+            const float oy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].y), 0xB1, 0xF, 0xF, false));
+            const int p = (j >> 1) + (TP / 2) * s;
+            float2 be = odd ? make_float2(ox, oy) : v[s], bo = odd ? v[s] : make_float2(ox, oy);
+            if (odd) {
+                be = cconj(be);
+                bo = cconj(bo);
+            }
+            if (self) {
+                be.y = 0.f;
+                bo.y = 0.f;
+            }
+            if (!(odd && self)) PR[(odd ? km : kx) * SP + p] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+    }
+    __syncthreads();
+
+    // I: row pair p's packed spectrum -> inverse row FFT -> zin (x on the last iteration)
+    float* out = a.o0 + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) v[k1] = PR[(j + TQ * k1) * SP + p];
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            out[(2 * p) * L + j + TP * s] = v[s].x;
+            out[(2 * p + 1) * L + j + TP * s] = v[s].y;
+        }
+    }
+}
 // ---------------------------------------------------------------- fused small-image Gaussian init
 // L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
 // G = conj(H) F(max(y,0)/alpha), and F(x0) into the W~ slot (iteration 0 forms W~1 from it, see w1_value)
@@ -2817,6 +2911,22 @@ struct Ops {
         });
     }
 };
+
+// the launch the runtime-planned Gaussian iteration uses at 160^2 (GOps::admm_iter_gauss)
+inline int gal_mid_launch(const Args& a, hipStream_t st) {
+    constexpr int L = 160, NT = 512;
+    static const char* names[4] = {"k_gal_mid<160,MID>", "k_gal_mid<160,FIRST>", "k_gal_mid<160,LAST>",
+                                   "k_gal_mid<160,FIRST_LAST>"};
+    ProfScope ps(names[a.first + 2 * a.last], st);
+    if (a.first) {
+        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, true, true>), dim3(a.N), dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, true, false>), dim3(a.N), dim3(NT), 0, st, a);
+    } else {
+        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, false, true>), dim3(a.N), dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, false, false>), dim3(a.N), dim3(NT), 0, st, a);
+    }
+    return check_launch("k_gal_mid");
+}
 
 #include "gd_generic.hpp"  // GOps: the same operations for any other H x W (runtime-planned line FFTs)
 

@@ -167,7 +167,7 @@ __device__ __forceinline__ c2 vtwmul(c2 v) {
 }
 
 // ---------------------------------------------------------------- in-register DFTs
-constexpr int first_factor(int n) { return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : 3); }
+constexpr int first_factor(int n) { return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : (n % 3 == 0 ? 3 : 5)); }
 
 template <int N, bool INV>
 struct DFT {
@@ -230,6 +230,23 @@ struct DFT<3, INV> {
         x[0] = x[0] + t1;
         x[1] = add_mi<INV>(t2, d);
         x[2] = add_mi<!INV>(t2, d);
+    }
+};
+
+template <bool INV>
+struct DFT<5, INV> {
+    // forward X1 = a1 - i b1, X4 = a1 + i b1, X2 = a2 - i b2, X3 = a2 + i b2 (c_k = cos(2 pi k / 5), s_k = sin)
+    __device__ __forceinline__ static void run(c2 (&x)[5]) {
+        constexpr float c1 = 0.309016994374947424102293417182819059f, c2k = -0.809016994374947424102293417182819059f;
+        constexpr float s1 = 0.951056516295153572116439333379382143f, s2 = 0.587785252292473129168705954639072769f;
+        const c2 t1 = x[1] + x[4], t2 = x[2] + x[3], t3 = x[1] - x[4], t4 = x[2] - x[3];
+        const c2 a1 = x[0] + c1 * t1 + c2k * t2, a2 = x[0] + c2k * t1 + c1 * t2;
+        const c2 b1 = s1 * t3 + s2 * t4, b2 = s2 * t3 - s1 * t4;
+        x[0] = x[0] + t1 + t2;
+        x[1] = add_mi<INV>(a1, b1);
+        x[4] = add_mi<!INV>(a1, b1);
+        x[2] = add_mi<INV>(a2, b2);
+        x[3] = add_mi<!INV>(a2, b2);
     }
 };
 

@@ -748,6 +748,9 @@ struct GOps {
         });
     }
     static int admm_iter_gauss(Args a, hipStream_t st0) {
+        // 160^2: the whole iteration in one workgroup per galaxy (k_gal_mid; the same state layout and per-bin
+        // arithmetic as this chain)
+        if (GD_MID_FUSED && g_fused && a.gH == 160 && a.gW == 160) return gal_mid_launch(a, st0);
         return chunks(a, st0, [&](const Args& b, hipStream_t st) {
             GD_TRY(Lc::rf<RF_ONE>(b, st));
             if (b.first)

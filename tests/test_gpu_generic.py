@@ -289,3 +289,32 @@ def test_generic_batch_invariance_and_odd_batch(dev):
         assert torch.equal(rl[i:i + 1], engine.richardson_lucy(obs[i:i + 1], psf[i:i + 1], 3).cpu())
     ref = O.wiener(obs[:2].cpu(), psf[:2].cpu(), alpha[:2].cpu())
     assert nerr(full[:2], ref) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 2, 4])
+def test_generic_fused_160_matches_chain_and_oracle(dev, n):
+    """160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum in LDS, 16-lane x
+    10-point line transforms) against the runtime-planned three-kernel chain (gd_set_fused_iteration(0)) and the
+    fp64-capable oracle, over first / middle / last / first-and-last iterations, ragged batch of 5."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 5
+    obs, psf, alpha, _ = make_batch(N, 160, h=48, seed=41 + n, device=dev)
+    gen = torch.Generator().manual_seed(77 + n)
+    rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
+    rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
+    m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
+    with torch.no_grad():
+        out_f = m(obs, psf, alpha).cpu()
+        old = lib.gd_set_fused_iteration(0)
+        try:
+            out_c = m(obs, psf, alpha).cpu()
+        finally:
+            lib.gd_set_fused_iteration(old)
+    ref = O.admm_forward(obs.cpu().double(), psf.cpu().double(), alpha.cpu().double(), rho1.double(), rho2.double(),
+                         "Gaussian")
+    e_fc, e_f, e_c = nerr(out_f, out_c), nerr(out_f, ref), nerr(out_c, ref)
+    print(f"160^2 n={n}: fused vs chain {e_fc:.2e}, vs fp64 oracle {e_f:.2e} (chain {e_c:.2e})")
+    assert e_fc < 5e-6
+    assert e_f < TOL and e_c < TOL

@@ -4,7 +4,7 @@
 # reading that traffic.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; export TMPDIR=/tmp; T=${1:-r04final}; mkdir -p $O
 B="python3 $R/bench.py --no-cpu-baseline --no-e2e --no-graph --no-ingest"
-cd $R && GD_PARITY_LOG=$O/parity_$T.jsonl timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
+cd $R && GD_PARITY_LOG=$O/parity_$T.jsonl timeout -k 10 500 python3 -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread ${PYTEST_DESELECT:+-k "$PYTEST_DESELECT"} > $O/gpu_tests_$T.log 2>&1 &&
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$T.txt 2>&1 &&
 cd /tmp && timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gd::" -d $O/pf_$T -o fetch --output-format csv -- $B --steps 1 --warmup 1 > /dev/null 2> $O/pmc_$T.err &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gd::" -d $O/pw_$T -o write --output-format csv -- $B --steps 1 --warmup 1 > /dev/null 2>> $O/pmc_$T.err &&
