@@ -2176,7 +2176,7 @@ __global__ __launch_bounds__(256) void k_gal_small_init(Args a) {
 // in each XCD's arrival order (block b runs on XCD b % 8; its q = b / 8-th arrival there), over a grid of
 // 2 roundup(N, 8); 2 = the roles alternate block by block.  Blocks of galaxies >= N return at once.
 template <int L>
-__global__ __launch_bounds__(subnet::kThreads) void k_subnet_rhos_init(Args a, const float* __restrict__ psf, long long psf_gstride,
+__global__ __launch_bounds__(subnet::kThreads, GD_SN_WPE) void k_subnet_rhos_init(Args a, const float* __restrict__ psf, long long psf_gstride,
                                                                         int h, const float* __restrict__ params,
                                                                         const float* __restrict__ mlp,
                                                                         const float* __restrict__ alpha,
@@ -2707,6 +2707,11 @@ int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
     if (G >= a.N) return f(a, st);
     int S = g_pipe_streams < kMaxPipe ? g_pipe_streams : kMaxPipe;
     if (S > a.N / G) S = a.N / G;  // regions must fit the caller's workspace
+    // Under stream capture the chunks go in sequence on the caller's stream: instantiating a graph that
+    // holds this fork / join (the same events recorded once per pipelined operation) crashed the ROCm 7
+    // runtime inside hipStreamEndCapture at 4096 x 160^2 (profiles/r04dbg_160_graph_crash.txt)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (S > 1 && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) S = 1;
     PipeRes* r = S > 1 ? pipe_res() : nullptr;
     if (!r) S = 1;
     std::unique_lock<std::mutex> lk;

@@ -698,6 +698,25 @@ __global__ __launch_bounds__(kMlpThreads) void k_subnet_mlp_mfma(const float* __
 // Cache: at a few hundred galaxies (one workgroup per CU) that costs ~2 us per galaxy, against a separate
 // batched launch of 32 workgroups (18 us at 256 x 48^2).
 static_assert(kThreads == kMlpThreads, "the fused kernel runs the MLP with the feature kernel's threads");
+#ifndef GD_SN_MLP2
+#define GD_SN_MLP2 1  // 0: the round-3 MLP of the one-launch SubNet (W1 slice loaded whole, W2 / W3 from L2 in the chains)
+#endif
+#ifndef GD_SN_WPE
+#define GD_SN_WPE 4  // waves per SIMD the one-launch kernels are compiled for: two 512-thread workgroups per CU
+#endif
+#ifndef GD_SN_MLP2_CH
+#define GD_SN_MLP2_CH 16  // W1 rows per chunk (two chunks in flight)
+#endif
+// a value the compiler cannot see through: loads addressed from it stay after this point (the W1 chunks
+// were otherwise all hoisted to the MLP's start and spilled)
+__device__ __forceinline__ int sn_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ float sn_opaquef(float v) {  // (and a chunk's FMAs complete before the next chunk)
+    asm volatile("" : "+v"(v));
+    return v;
+}
 // The kernels pass their own __restrict__ pointer arguments (read-only weights through a struct member
 // lose the no-alias proof that lets them be scalar loads: the SubNet ran 43 -> 58 us at 256 that way).
 __device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long long psf_gstride, int h,
@@ -717,6 +736,91 @@ __device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long lo
     const float* W3 = b2 + kHidden;
     const float* b3 = W3 + kHidden * n_out;
     const int o = tid % kHidden, q = tid / kHidden;  // q is wave-uniform
+#if GD_SN_MLP2
+    // W2 and W3 are staged in region B above the partial sums by all 512 threads: their loads are issued with
+    // layer 1's last W1 chunk, so they land while layer 1 computes, and layers 2 and 3 (wave 0, chains over
+    // 64 inputs) read each lane's weight column from LDS in one batch instead of waiting on L2 every 8 inputs.  Layer 1 streams W1 in 4 chunks of 32
+    // rows, chunk c + 1 in flight while chunk c's FMAs issue.  Every sum keeps its order.
+    float* W2s = P + 1024;                 // [64][64]
+    float* W3s = W2s + kHidden * kHidden;  // [64][n_out]
+    constexpr int N2 = kHidden * kHidden / kThreads, N3 = kHidden * kMaxOut / kThreads;
+    static_assert(N2 * kThreads == kHidden * kHidden && 1024 + kHidden * (kHidden + kMaxOut) <= kRegionB, "W2, W3 in region B");
+    const int n3 = kHidden * n_out;
+    float w2r[N2], w3r[N3], bo[3];
+    {
+        constexpr int CH = GD_SN_MLP2_CH, NCH = kMlpKQ / CH;
+        const int i0 = q * kMlpKQ;
+        const float* wp = W1 + (size_t)i0 * kHidden + o;
+        float part = 0.f;
+        float wb[2][CH];
+        {
+            const float* wc = wp + sn_opaque(0);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) wb[0][k] = wc[k * kHidden];
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c + 1 < NCH) {
+                const float* wc = wp + sn_opaque(CH * (c + 1) * kHidden);
+#pragma unroll
+                for (int k = 0; k < CH; ++k) wb[(c + 1) & 1][k] = wc[k * kHidden];
+            }
+            if (c + 2 == NCH) {  // after the last W1 chunk: waiting for a chunk never waits for these
+#pragma unroll
+                for (int e = 0; e < N2; ++e) w2r[e] = W2[tid + e * kThreads];
+#pragma unroll
+                for (int e = 0; e < N3; ++e) w3r[e] = tid + e * kThreads < n3 ? W3[tid + e * kThreads] : 0.f;
+                bo[0] = b1[o];
+                bo[1] = b2[o];
+                bo[2] = o < n_out ? b3[o] : 0.f;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const float* xc = X + i0 + sn_opaque(CH * c);  // (the LDS reads were hoisted whole as well)
+#pragma unroll
+            for (int k = 0; k < CH; ++k) part = fmaf(wb[c & 1][k], xc[k], part);
+            part = sn_opaquef(part);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (q == kMlpWaves - 1) part = fmaf(W1[kFeat * kHidden + o], xa, part);
+        P[q * kHidden + o] = part;
+#pragma unroll
+        for (int e = 0; e < N2; ++e) W2s[tid + e * kThreads] = w2r[e];
+#pragma unroll
+        for (int e = 0; e < N3; ++e)
+            if (tid + e * kThreads < n3) W3s[tid + e * kThreads] = w3r[e];
+    }
+    __syncthreads();
+    SN_TRACE(11);
+    if (q == 0) {
+        // layers 2 and 3 in wave 0: lane o holds h1[o] (h2[o]); input i of the chain is lane i's value, broadcast
+        // with v_readlane; the 64 weights of the lane's output column come from LDS in one batch of reads
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < kMlpWaves; ++w) v += P[w * kHidden + o];
+        const float h1 = fmaxf(v + bo[0], 0.f);
+        float wc[kHidden];
+#pragma unroll
+        for (int i = 0; i < kHidden; ++i) wc[i] = W2s[i * kHidden + o];
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kHidden; ++i)
+            acc = fmaf(wc[i], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h1), i)), acc);
+        const float h2 = fmaxf(acc + bo[1], 0.f);
+        const int o3 = o < n_out ? o : 0;
+#pragma unroll
+        for (int i = 0; i < kHidden; ++i) wc[i] = W3s[i * n_out + o3];
+        acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < kHidden; ++i)
+            acc = fmaf(wc[i], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h2), i)), acc);
+        if (o < n_out) {
+            const float v3 = acc + bo[2];
+            // nn.Softplus(beta = 1, threshold = 20), then + 1e-6 (:86)
+            rhos[(size_t)g * n_out + o] = (v3 > 20.f ? v3 : log1pf(expf(v3))) + 1e-6f;
+        }
+    }
+    SN_TRACE(12);
+#else
     {
         const int i0 = q * kMlpKQ;
         float wv[kMlpKQ];
@@ -753,8 +857,9 @@ __device__ __forceinline__ void rhos_body(const float* __restrict__ psf, long lo
         }
     }
     SN_TRACE(11);
+#endif
 }
-__global__ __launch_bounds__(kThreads) void k_subnet_rhos_psf(const float* __restrict__ psf, long long psf_gstride,
+__global__ __launch_bounds__(kThreads, GD_SN_WPE) void k_subnet_rhos_psf(const float* __restrict__ psf, long long psf_gstride,
                                                              int h, const float* __restrict__ params,
                                                              const float* __restrict__ mlp,
                                                              const float* __restrict__ alpha, long long alpha_stride,

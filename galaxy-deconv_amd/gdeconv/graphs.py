@@ -4,8 +4,10 @@ The reference runs every forward eagerly from Python (``test.py:237``).  At LSST
 a few hundred galaxies) one ``Unrolled_ADMM`` forward is a chain of ~60 short launches - SubNet,
 OTF, init_l2, 8 x (denoiser, spectral iteration) - and the host, not the GPU, sets the pace.
 ``GraphedForward`` records the forward once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm)
-and replays it: the engine's C ABI enqueues on torch's current stream, allocates nothing of its own
-and forks its Infinity-Cache pipeline onto internal streams with events, all of which capture.
+and replays it: the engine's C ABI enqueues on torch's current stream and allocates nothing of its
+own; under capture its Infinity-Cache chunks run in sequence on that stream (the eager path forks them
+onto internal streams with events - a fork / join the ROCm 7 runtime crashed on when instantiating the
+graph, ``profiles/r04dbg_160_graph_crash.txt``).
 
     g = GraphedForward(model, obs, psf, alpha)     # shapes fixed at capture
     rec = g(obs2, psf2, alpha2)                    # copies inputs in, replays, returns the output

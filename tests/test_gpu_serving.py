@@ -52,6 +52,28 @@ def test_graphed_forward_engine_bit_identical(dev, L, N, llh):
     assert torch.equal(g(obs2, psf2, alpha2), eager2)
 
 
+@pytest.mark.parametrize("L", [80, 160])
+def test_graphed_forward_chunked_pipeline(dev, L):
+    """A forward whose runtime-planned operations run in several Infinity-Cache chunks (chunk bytes
+    forced down to two galaxies; 4096 x 160^2 in the bench does the same at 96 MiB) captures and
+    replays bit-identically; the chunks go in sequence under capture."""
+    from gdeconv import _lib
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    tgal = 2 * (L // 2 + 1) * L * 8
+    old = lib.gd_set_chunk_bytes(2 * tgal)
+    try:
+        m = _model(8, "Gaussian", dev, identity=True)
+        obs, psf, alpha, _ = make_batch(7, L, seed=11, device=dev)
+        with torch.no_grad():
+            eager = m(obs, psf, alpha)
+        g = GraphedForward(m, obs, psf, alpha, clone=True)
+        assert torch.equal(g(obs, psf, alpha), eager)
+    finally:
+        lib.gd_set_chunk_bytes(old)
+
+
 def test_graphed_forward_full_model(dev):
     """Whole model incl. SubNet and the ResUNet denoiser, captured at 48^2."""
     from gdeconv.graphs import GraphedForward

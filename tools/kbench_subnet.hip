@@ -28,10 +28,10 @@ static std::vector<float> rnd(size_t n, float scale, unsigned seed) {
     return v;
 }
 
-static const char* kPhase[12] = {"start", "PSF rows+cols FFT", "|H|^2 pool", "conv0 1->4 @64",
+static const char* kPhase[13] = {"start", "PSF rows+cols FFT", "|H|^2 pool", "conv0 1->4 @64",
                                  "conv1 4->4 @64+pool", "conv2 4->8 @32", "conv3 8->8 @32+pool",
                                  "conv4 8->16 @16", "conv5 16->16 @16+pool", "conv6 16->16 @8",
-                                 "conv7 16->16 @8", "MLP"};
+                                 "conv7 16->16 @8", "MLP (layer 1)", "MLP layers 2-3"};
 
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096, Nr = argc > 2 ? atoi(argv[2]) : 256,
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(t.data(), tr, t.size() * 8, hipMemcpyDeviceToHost));
         printf("  phase trace (mean us per workgroup, 100 MHz clock):\n");
-        for (int k = 1; k < 12; ++k) {
+        for (int k = 1; k < 13; ++k) {
             double s = 0;
             int c = 0;
             for (int g = 0; g < n; ++g)
@@ -98,7 +98,7 @@ int main(int argc, char** argv) {
             if (c) printf("    %-24s %8.2f\n", kPhase[k], s / c * 1e-2);
         }
         double s = 0;
-        for (int g = 0; g < n; ++g) s += double(t[g * 16 + (t[g * 16 + 11] ? 11 : 10)] - t[g * 16]);
+        for (int g = 0; g < n; ++g) s += double(t[g * 16 + (t[g * 16 + 12] ? 12 : t[g * 16 + 11] ? 11 : 10)] - t[g * 16]);
         printf("    %-24s %8.2f\n", "whole workgroup", s / n * 1e-2);
 #endif
     };

@@ -39,7 +39,7 @@ def pretty(kname):
     m = re.search(r"k_subnet_rhos_init<(\d+)>", kname)
     if m:
         return f"k_subnet_rhos_init<{m.group(1)}>"   # SubNet + the small-image init in one launch
-    m = re.search(r"k_gal_small_t<(\d+), \d+, \d+, (true|false), (true|false)>", kname)
+    m = re.search(r"k_gal_(?:small_t|small_p|mid)<(\d+), \d+, \d+(?:, \d+)?, (true|false), (true|false)>", kname)
     if m:  # the transposing-plan small-image iteration: same role (and names) as k_gal_small
         first, last = m.group(2) == "true", m.group(3) == "true"
         return f"k_gal_small<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
@@ -103,10 +103,12 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--iters", type=int, default=16,
-                    help="ADMM iterations in the profiled run (bench --steps 1 --warmup 1: 2 x 8)")
+    ap.add_argument("--iters", type=int, default=None,
+                    help="ADMM iterations in the profiled run (default: the init kernel's launches x --n-iters; "
+                         "bench --steps 1 --warmup 1 runs 3 forwards: warmup, timed region, profiling pass)")
     ap.add_argument("--rl-calls", type=int, default=0,
-                    help="Richardson-Lucy workload: forwards in the profiled run (bench --steps 1 --warmup 1: 2); "
+                    help="Richardson-Lucy workload (any value > 0 selects it): forwards in the profiled run, "
+                         "overridden by the k_rl_reg launch count when that kernel ran; "
                          "op_richardson_lucy<L> = every engine kernel's bytes / calls")
     ap.add_argument("--n-iters", type=int, default=None, help="iterations per forward of the profiled workload")
     a = ap.parse_args()
@@ -127,6 +129,14 @@ def main():
                              "hbm_bytes_per_launch": rd + wr, "launches": nf.get(k, 0)}
     # whole Gaussian ADMM iteration (RF(z) -> C_G_ITER[0] -> RI(zin), all chunks): traffic per call
     L = a.size
+    if a.iters is None:  # forwards in the run = launches of the one-per-forward init kernel
+        fw = 0
+        for k in (f"k_gal_init<{L},REG>", f"k_gal_init<{L},POIS>", f"k_gal_small_init<{L}>",
+                  f"k_subnet_rhos_init<{L}>", f"k_gal_init<{L},ONE>", f"k_gal_init<{L},W1>"):
+            fw = fw or out["kernels"].get(k, {}).get("launches", 0)
+        a.iters = fw * (a.n_iters or 8) if fw else 24
+    if a.rl_calls and f"k_rl_reg<{L}>" in out["kernels"]:
+        a.rl_calls = out["kernels"][f"k_rl_reg<{L}>"]["launches"]
     members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER_F>", f"k_col<{L},G_ITER_L>",
                f"k_row_inv<{L},OUT1>", f"k_gal_iter<{L},MID>", f"k_gal_iter<{L},FIRST>", f"k_gal_iter<{L},LAST>",
                f"k_gal_reg<{L}>", f"k_gal_small<{L},MID>", f"k_gal_small<{L},FIRST>", f"k_gal_small<{L},LAST>",
