@@ -101,7 +101,8 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         = 2 img + 5.5 half (first: no U1 read, 4.5; last: no G read, nothing written, 2.5; first-and-last
         at 256^2 reads G to form W~1, 2.5); three-kernel: + the RF / C / RI workspace round trips.
       op_admm_init, Gaussian, fused: y + PSF in, |H|^2, G, W~ (or F(x0)) + zin out = 2 img + 2.5 half
-        + the PSF (h^2 floats) and at 256^2 its compact row spectra (h (L/2 + 1) complex, written and read)."""
+        + the PSF (h^2 floats) and at 256^2 its compact row spectra (h (L/2 + 1) complex, written and read; at
+        160^2 the packed row-pair spectra, h/2 x L complex)."""
     img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
     k = pretty(name)
     if k == f"op_richardson_lucy<{L}>":
@@ -117,7 +118,8 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
     if k == f"op_admm_init<{L},Gaussian>" and fused:
         # k_psf_rows<STATE>'s compact row spectra [kx][i] (h (L/2 + 1) complex), written once and read once; the
         # round-3 model counted them twice over (5.70 GB at 4096 x 256^2 against PMC 5.32 GB = 0.93x; now 5.30 GB)
-        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else 0
+        # (160^2, k_gal_mid_init: the PSF's packed row-pair spectra [L][h/2] parked in the U1 slot, written and read)
+        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L == 160 else 0)
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:
@@ -611,7 +613,9 @@ def main():
                             (("k_psf_rows + k_gal_reg_init<POIS>" if fused_init else "chunked Gaussian chain")
                              + " + k_pois_b<INIT>") if pois2 else
                             ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
-                             and not generic else "chunked" + (", runtime-planned line FFTs" if generic else "")))},
+                             and not generic else
+                             "fused, k_gal_mid_init (160^2: one launch, half spectrum in LDS)" if mid_fused and fused_init
+                             else "chunked" + (", runtime-planned line FFTs" if generic else "")))},
         "roofline": roofline,
         # SURVEY.md 8(d)'s per-galaxy byte model prices the reference's op-for-op path (16 fp32 words per
         # pixel per iteration); this engine's compulsory traffic is 7.5 (roofline above), so the survey

@@ -2059,6 +2059,165 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
         }
     }
 }
+// ---------------------------------------------------------------- fused Gaussian init at 160^2
+// init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants and F(x0) in one launch, one 512-thread
+// workgroup per galaxy on k_gal_mid's layout: the runtime-planned chain RF_PSF_Y -> C_G_INIT -> RIF_CLAMP ->
+// C_G_W1 (four launches through the chunked workspace), bin for bin:
+//   P  the placed PSF's row pairs (psf_to_otf's circular placement, gpsf) -> FFT -> packed spectra, parked
+//      in the galaxy's U1 slot as [kx][pair] (the slot is not read before iteration 0 writes it)
+//   R  max(y, 0) / alpha row pairs -> FFT -> PR
+//   C  per column kx: the OTF column (rows separated from the parked spectra, FFT) and Y's (from PR);
+//      |H|^2, G = conj(H) Y -> state; X0 = G / (|H|^2 + 1/alpha) / L^2; IFFT -> PR (packed, in place)
+//   I  row pairs: IFFT -> x0 = clamp(., 0, 1) -> zin; FFT -> PR
+//   W  per column: FFT -> F(x0) -> the W~ slot (iteration 0 forms W~1 from it, w1_value)
+template <int L, int TP, int TQ, int NT>
+__global__ __launch_bounds__(NT) void k_gal_mid_init(Args a) {
+    constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1;
+    constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    static_assert(TP * TQ == L && TP >= TQ && TP % 2 == 0 && NT % G == 0, "lines of TP lanes, rows paired per lane");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 PR[L * SP];
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, NT);
+    const int h = a.h, h2 = h >> 1, npp = (h + 1) >> 1;
+    const float al = a.alpha(g);
+    const float ial = 1.0f / al;  // the chain's lhs = |H|^2 + 1.0f / alpha
+    const float* psf = a.psf + (long long)g * a.psf_gstride;
+    float2* pc = a.s_u1 + (size_t)g * K * L;  // parked PSF spectra [kx][pair], L npp <= K L
+    __syncthreads();
+    float2 v[G];
+
+    // P: PSF rows 2p, 2p + 1 placed on the L-point circle (column c holds PSF column (c + h/2) mod L when < h)
+    for (int p = line; p < npp; p += LINES) {
+        const int i0 = 2 * p, i1 = i0 + 1;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            int jj = j + TP * s + h2;
+            if (jj >= L) jj -= L;
+            const bool in = jj < h;
+            v[s] = make_float2(in ? psf[i0 * h + jj] : 0.f, (in && i1 < h) ? psf[i1 * h + jj] : 0.f);
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) pc[(j + TQ * k1) * npp + p] = v[k1];
+        }
+    }
+    // R: max(y, 0) / alpha (RF_PSF_Y's slot 1)
+    const float* y = a.y + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+#pragma unroll
+        for (int s = 0; s < TQ; ++s)
+            v[s] = make_float2(fmaxf(y[(2 * p) * L + j + TP * s], 0.f) / al, fmaxf(y[(2 * p + 1) * L + j + TP * s], 0.f) / al);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[(j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();  // PR complete, the parked PSF spectra visible to the workgroup
+
+    const bool odd = j & 1, cl = j < TQ;
+    // C: column kx; lane j holds rows r = j + TP s (pair (j >> 1) + (TP / 2) s, parity j & 1)
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+        float2 hv[G];
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[kx * SP + p], Dm = PR[km * SP + p];
+            v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+            int i = j + TP * s + h2;  // padded row r -> PSF row (r + h/2) mod L (gpsf)
+            if (i >= L) i -= L;
+            float2 hval = make_float2(0.f, 0.f);
+            if (i < h) {
+                const float2 Cp = pc[kx * npp + (i >> 1)], Dp = pc[km * npp + (i >> 1)];
+                hval = (i & 1) ? make_float2(0.5f * (Cp.y + Dp.y), 0.5f * (Dp.x - Cp.x))
+                               : make_float2(0.5f * (Cp.x + Dp.x), 0.5f * (Cp.y - Dp.y));
+            }
+            hv[s] = hval;
+        }
+#pragma unroll
+        for (int s = TQ; s < G; ++s) hv[s] = make_float2(0.f, 0.f);
+        tline_fft<L, TP, TQ, false>(hv, j, my, tw);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) {
+            const float2 Hk = hv[k1], Yk = v[k1];
+            const float hh = Hk.x * Hk.x + Hk.y * Hk.y;  // C_G_INIT's arithmetic
+            const float2 Gk = cmulc(Yk, Hk);
+            if (cl) {
+                a.s_hh[ob + TQ * k1] = hh;
+                a.s_g[ob + TQ * k1] = Gk;
+            }
+            const float lhs = hh + ial;
+            v[k1] = cscale(make_float2(Gk.x / lhs, Gk.y / lhs), inv_n);
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        const bool self = (kx == 0) || (2 * kx == L);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {  // the next row phase's packed input (k_gal_mid)
+            const float ox = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].x), 0xB1, 0xF, 0xF, false));
+            const float oy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[s].y), 0xB1, 0xF, 0xF, false));
+            const int p = (j >> 1) + (TP / 2) * s;
+            float2 be = odd ? make_float2(ox, oy) : v[s], bo = odd ? v[s] : make_float2(ox, oy);
+            if (odd) {
+                be = cconj(be);
+                bo = cconj(bo);
+            }
+            if (self) {
+                be.y = 0.f;
+                bo.y = 0.f;
+            }
+            if (!(odd && self)) PR[(odd ? km : kx) * SP + p] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+    }
+    __syncthreads();
+
+    // I: IFFT -> x0 = clamp(x0, 0, 1) -> zin (RIF_CLAMP); FFT of the clamped rows -> PR
+    float* out = a.o2 + (size_t)g * L * L;
+    for (int p = line; p < L / 2; p += LINES) {
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) v[k1] = PR[(j + TQ * k1) * SP + p];
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            v[s] = make_float2(fminf(fmaxf(v[s].x, 0.f), 1.f), fminf(fmaxf(v[s].y, 0.f), 1.f));
+            out[(2 * p) * L + j + TP * s] = v[s].x;
+            out[(2 * p + 1) * L + j + TP * s] = v[s].y;
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[(j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();
+
+    // W: F(x0)'s columns -> the W~ slot (C_G_W1)
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[kx * SP + p], Dm = PR[km * SP + p];
+            v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (cl) {
+            const size_t ob = ((size_t)g * K + kx) * L + j;
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) a.s_w[ob + TQ * k1] = v[k1];
+        }
+    }
+}
 // ---------------------------------------------------------------- fused small-image Gaussian init
 // L <= 96: init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants |H|^2 and
 // G = conj(H) F(max(y,0)/alpha), and F(x0) into the W~ slot (iteration 0 forms W~1 from it, see w1_value)
@@ -2931,6 +3090,13 @@ inline int gal_mid_launch(const Args& a, hipStream_t st) {
         else hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, false, false>), dim3(a.N), dim3(NT), 0, st, a);
     }
     return check_launch("k_gal_mid");
+}
+
+inline int gal_mid_init_launch(const Args& a, hipStream_t st) {
+    constexpr int L = 160, NT = 512;
+    ProfScope ps("k_gal_mid_init<160>", st);
+    hipLaunchKernelGGL((k_gal_mid_init<L, 16, 10, NT>), dim3(a.N), dim3(NT), 0, st, a);
+    return check_launch("k_gal_mid_init");
 }
 
 #include "gd_generic.hpp"  // GOps: the same operations for any other H x W (runtime-planned line FFTs)

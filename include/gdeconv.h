@@ -240,7 +240,10 @@ int gd_set_subnet_fused_max(int n);
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->
  * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic.  on: 1 = k_gal_reg_init
  * (default, one launch), 2 = k_gal_iter<KM=1> + k_gal_w1 (two launches), 3 = k_gal_iter<KM=3> (one
- * launch, 1024 threads); 0 selects the chunked chain.  Returns the previous setting; process-wide. */
+ * launch, 1024 threads); 0 selects the chunked chain.  At 160^2 any non-zero value selects k_gal_mid_init
+ * (one launch: the placed PSF's row spectra parked in the U1 slot, the half spectrum in LDS) in place of
+ * the runtime-planned RF_PSF_Y -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain.  Returns the previous setting;
+ * process-wide. */
 int gd_set_fused_init(int on);
 
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,

@@ -291,11 +291,12 @@ def test_generic_batch_invariance_and_odd_batch(dev):
     assert nerr(full[:2], ref) < TOL
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [0, 1, 2, 4])
 def test_generic_fused_160_matches_chain_and_oracle(dev, n):
     """160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum in LDS, 16-lane x
-    10-point line transforms) against the runtime-planned three-kernel chain (gd_set_fused_iteration(0)) and the
-    fp64-capable oracle, over first / middle / last / first-and-last iterations, ragged batch of 5."""
+    10-point line transforms) and the init in one launch (k_gal_mid_init) against the runtime-planned chains
+    (gd_set_fused_iteration(0), gd_set_fused_init(0)) and the fp64-capable oracle: n = 0 is init_l2 alone (x0),
+    then first / middle / last / first-and-last iterations, ragged batch of 5."""
     from gdeconv import _lib
     from gdeconv.synth import make_batch
     lib = _lib.load()
@@ -307,11 +308,12 @@ def test_generic_fused_160_matches_chain_and_oracle(dev, n):
     m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
     with torch.no_grad():
         out_f = m(obs, psf, alpha).cpu()
-        old = lib.gd_set_fused_iteration(0)
+        old, old_i = lib.gd_set_fused_iteration(0), lib.gd_set_fused_init(0)
         try:
             out_c = m(obs, psf, alpha).cpu()
         finally:
             lib.gd_set_fused_iteration(old)
+            lib.gd_set_fused_init(old_i)
     ref = O.admm_forward(obs.cpu().double(), psf.cpu().double(), alpha.cpu().double(), rho1.double(), rho2.double(),
                          "Gaussian")
     e_fc, e_f, e_c = nerr(out_f, out_c), nerr(out_f, ref), nerr(out_c, ref)
