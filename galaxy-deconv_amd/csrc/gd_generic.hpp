@@ -1,4 +1,4 @@
-// gd_generic.hpp - the runtime-size path: any H x W image with 2 <= H, W <= 1024, square or not.
+// gd_generic.hpp - the runtime-size path: any H x W image with 2 <= H, W <= 1638, square or not.
 //
 // The specialised sizes (square 32, 48, 64, 96, 128, 256) run the compile-time-planned kernels of
 // gd_engine.hip.  Every other size the reference's torch.fft path accepts (utils/utils_torch.py:22-27,
@@ -22,7 +22,7 @@
 
 namespace gen {
 
-constexpr int kMaxLen = 1024;     // per axis
+constexpr int kMaxLen = 1638;     // per axis: a two-image workgroup (one line each, plus the ping-pong buffers), 5 n float2, in 64 KiB of LDS
 constexpr int kMaxStages = 16;
 constexpr int kThreads = 256;
 constexpr int kLdsFloat2 = 8192;  // 64 KiB

@@ -7,7 +7,7 @@ library raises (``gdeconv._lib.EngineError``).
 Layouts: images fp32 [N,1,H,W] contiguous (NCHW, C=1, as in the reference); the OTF is the
 half spectrum stored transposed, complex64 [N, W//2+1, H] (``otf[g, kx, ky]``).
 
-Sizes: any H x W with 2 <= H, W <= 1024 (square or not).  Square 32/48/64/96/128/256 run the
+Sizes: any H x W with 2 <= H, W <= 1638 (square or not).  Square 32/48/64/96/128/256 run the
 compile-time-planned kernels (and the fused whole-galaxy kernels at 256^2 / <= 128); every other
 size runs the runtime-planned kernels of ``csrc/gd_generic.hpp`` with the same operation chains
 (``supported(H, W)`` returns 1 resp. 2).
@@ -101,7 +101,7 @@ def workspace(N, H, W, device):
     reuse is stream-ordered; nothing is shared across streams or threads)."""
     lib = _lib.load()
     if not lib.gd_supported_size(H, W):
-        raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 1024])")
+        raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 1638])")
     nbytes = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
@@ -550,7 +550,7 @@ class ADMMState:
             raise ValueError("llh must be 'Gaussian' or 'Poisson'")
         self.llh = _lib.GD_LLH[llh]
         if not self.lib.gd_supported_size(self.H, self.W):
-            raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 1024])")
+            raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 1638])")
         nbytes = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W, self.llh))
         with _on(self.dev):
             self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160), (45, 61), (255, 255)]   # sizes.npz (odd W last)
 FFT_SIZES = [(2, 2), (3, 5), (17, 19), (40, 40), (64, 48), (45, 60), (97, 80), (243, 125), (1000, 30),
-             (7, 1024), (1024, 1024), (96, 256), (256, 255)]
+             (7, 1024), (1024, 1024), (96, 256), (256, 255), (1638, 1200), (1536, 1638), (1025, 1637)]
 
 
 def T(a):
@@ -289,6 +289,26 @@ def test_generic_batch_invariance_and_odd_batch(dev):
         assert torch.equal(rl[i:i + 1], engine.richardson_lucy(obs[i:i + 1], psf[i:i + 1], 3).cpu())
     ref = O.wiener(obs[:2].cpu(), psf[:2].cpu(), alpha[:2].cpu())
     assert nerr(full[:2], ref) < TOL
+
+
+@pytest.mark.parametrize("H,W", [(1638, 1536), (1200, 1400)])
+def test_generic_large_images_admm_and_wiener(dev, H, W):
+    """The largest images the runtime-planned path takes (1638 per side: a two-image workgroup's lines in
+    64 KiB of LDS): Wiener and Unrolled_ADMM(2, Gaussian) with an identity denoiser against the fp64 oracle."""
+    from gdeconv import engine
+    from gdeconv.synth import make_batch
+    obs, psf, alpha, _ = make_batch(1, H, W, h=48, seed=H + W)
+    wien = engine.wiener(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    assert nerr(wien, O.wiener(obs.double(), psf.double(), alpha.double())) < TOL
+    rho1 = torch.full((1, 1, 1, 2), 0.9)
+    rho2 = torch.full((1, 1, 1, 2), 1.1)
+    m = _spectral_model(2, "Gaussian", dev, rho1, rho2)
+    with torch.no_grad():
+        out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    ref = O.admm_forward(obs.double(), psf.double(), alpha.double(), rho1.double(), rho2.double(), "Gaussian")
+    e = nerr(out, ref)
+    print(f"{H}x{W}: Wiener / ADMM(2) vs fp64 oracle, ADMM {e:.2e}")
+    assert e < TOL
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 4])
