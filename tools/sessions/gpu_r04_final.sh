@@ -15,10 +15,13 @@ timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gd::" -d $O
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gd::" -d $O/pf48_$T -o fetch --output-format csv -- $B --size 48 --batch 256 --steps 1 --warmup 1 > /dev/null 2>> $O/pmc_$T.err &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gd::" -d $O/pw48_$T -o write --output-format csv -- $B --size 48 --batch 256 --steps 1 --warmup 1 > /dev/null 2>> $O/pmc_$T.err &&
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/ps_$T -o run --output-format csv -- $B --steps 3 --warmup 1 > $O/bench_stats_$T.json 2>> $O/pmc_$T.err &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/ps48_$T -o run --output-format csv -- $B --size 48 --batch 256 --steps 20 --warmup 2 > $O/bench48_stats_$T.json 2>> $O/pmc_$T.err &&
+timeout -k 10 120 rocprofv3 --kernel-trace -d $O/gt48_$T -o run --output-format csv -- python3 $R/tools/graph_trace.py 20 256 48 > $O/gt48_$T.txt 2>> $O/pmc_$T.err &&
 cd $R && python3 tools/pmc_summary.py $O/pf_$T/fetch_counter_collection.csv $O/pw_$T/write_counter_collection.csv $O/pmc_traffic_$T.json --batch 4096 --size 256 --n-iters 8 > $O/pmc_summary_$T.txt 2>&1 &&
 python3 tools/pmc_summary.py $O/pfp_$T/fetch_counter_collection.csv $O/pwp_$T/write_counter_collection.csv $O/pmc_traffic_poisson_$T.json --batch 4096 --size 256 --n-iters 8 > $O/pmc_summary_poisson_$T.txt 2>&1 &&
-python3 tools/pmc_summary.py $O/pfrl_$T/fetch_counter_collection.csv $O/pwrl_$T/write_counter_collection.csv $O/pmc_traffic_rl_$T.json --batch 4096 --size 256 --rl-calls 2 --n-iters 100 > $O/pmc_summary_rl_$T.txt 2>&1 &&
+python3 tools/pmc_summary.py $O/pfrl_$T/fetch_counter_collection.csv $O/pwrl_$T/write_counter_collection.csv $O/pmc_traffic_rl_$T.json --batch 4096 --size 256 --rl-calls 1 --n-iters 100 > $O/pmc_summary_rl_$T.txt 2>&1 &&
 python3 tools/pmc_summary.py $O/pf48_$T/fetch_counter_collection.csv $O/pw48_$T/write_counter_collection.csv $O/pmc_traffic48_$T.json --batch 256 --size 48 --n-iters 8 > $O/pmc_summary48_$T.txt 2>&1 &&
+python3 tools/graph_timeline.py $O/gt48_$T/run_kernel_trace.csv 0 10 >> $O/gt48_$T.txt 2>&1 &&
 timeout -k 10 400 python3 bench.py --traffic-json $O/pmc_traffic_$T.json > $O/bench_$T.json 2> $O/bench_$T.err &&
 timeout -k 10 300 python3 bench.py --size 48 --batch 256 --steps 200 --warmup 20 --no-e2e --no-ingest --traffic-json $O/pmc_traffic48_$T.json > $O/bench48_$T.json 2> $O/bench48_$T.err &&
 timeout -k 10 300 python3 bench.py --llh Poisson --no-e2e --no-ingest --no-graph --traffic-json $O/pmc_traffic_poisson_$T.json > $O/bench_poisson_$T.json 2> $O/bench_poisson_$T.err &&
