@@ -119,7 +119,7 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         # k_psf_rows<STATE>'s compact row spectra [kx][i] (h (L/2 + 1) complex), written once and read once; the
         # round-3 model counted them twice over (5.70 GB at 4096 x 256^2 against PMC 5.32 GB = 0.93x; now 5.30 GB)
         # (160^2, k_gal_mid_init: the PSF's packed row-pair spectra [L][h/2] parked in the U1 slot, written and read)
-        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L == 160 else 0)
+        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L in (80, 112, 144, 160) else 0)
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:
@@ -169,6 +169,33 @@ def kernel_bytes(name, L, n_iters):
         f"k_row_invfwd<{L},CLAMP>": 2 * half + img,                         # T -> zin, T
     }
     return table.get(k)
+
+
+def graph_iter_ms(obs, psf, alpha, dev, reps=64):
+    """Average device time of one middle Gaussian ADMM iteration (gd_admm_iter) without host gaps: ``reps``
+    launches on one state, z fixed, captured in a hipGraph and replayed between two HIP events."""
+    from gdeconv import engine
+    N = obs.shape[0]
+    with torch.no_grad():
+        st = engine.ADMMState(obs, psf, alpha, "Gaussian")
+        st.init(None)
+        r = engine.RhoSchedule(torch.ones(N, 1, 1, reps + 2, device=dev), N, dev)
+        z = st.zin.clone()
+        st.step(z, r[0], r[0], r[1])  # iteration 0 (FIRST) outside the graph
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            for i in range(1, reps + 1):
+                st.step(z, r[i], r[i], r[i + 1])
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
 
 
 def survey_bytes_per_galaxy(L, n, h=48):
@@ -360,8 +387,9 @@ def main():
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
     generic = args.size not in (32, 48, 64, 96, 128, 256)  # gd_supported_size == 2: gd_generic.hpp
-    # 160^2 (runtime-planned size) runs its Gaussian iterations fused too (k_gal_mid, gd_engine.hip)
-    mid_fused = bool(fused) and args.size == 160 and args.llh == "Gaussian"
+    # 80 / 112 / 144 / 160 (runtime-planned sizes) run their Gaussian iterations and init fused too (k_gal_mid,
+    # k_gal_mid_init: gd_engine.hip mid_size)
+    mid_fused = bool(fused) and args.size in (80, 112, 144, 160) and args.llh == "Gaussian"
     use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian"
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     if args.pipe_streams is not None:
@@ -549,6 +577,12 @@ def main():
         dom_raw = max(priced, key=lambda k: kern[k][0])
         dom_ms = kern[dom_raw][0] / kern[dom_raw][1]
         per_gal = kernel_bytes(dom_raw, L, n)
+    timing = "HIP events on the caller's stream around each call, profiling pass"
+    if (use_fused and not rl and dom_ms < 0.05 and pretty(dom_raw) == f"op_admm_iter<{L},Gaussian>"):
+        # a short op of a host-bound eager forward (48^2): the events also time the host's enqueue gaps, so
+        # the launch duration comes from back-to-back launches replayed as one hipGraph instead
+        dom_ms = graph_iter_ms(obs, psf, alpha, dev)
+        timing = "64 back-to-back middle iterations (gd_admm_iter) replayed as one hipGraph, HIP events around it"
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
     if args.traffic_json is None:
@@ -570,7 +604,7 @@ def main():
     roofline = {"bound": "hbm", "kernel": pretty(dom_raw), "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic, "algorithmic_bytes_per_launch": per_gal * N if per_gal else None,
-                "avg_launch_ms": dom_ms}
+                "avg_launch_ms": dom_ms, "timing": timing}
     survey_b = survey_rl_bytes_per_galaxy(L, n) if rl else survey_bytes_per_galaxy(L, n)
     if rl:
         metric = f"galaxies/sec ({L}x{L}, Richard_Lucy n_iters={n})"
@@ -599,7 +633,7 @@ def main():
                    "ranks_seen": world, "backend": backend or "none",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
-                                               "k_gal_mid (160^2: half spectrum in LDS, 512 threads per galaxy)"
+                                               f"k_gal_mid ({L}^2: half spectrum in LDS, 512 threads per galaxy)"
                                                if mid_fused else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
                                  if use_fused else (rl_impl if rl else
@@ -614,7 +648,7 @@ def main():
                              + " + k_pois_b<INIT>") if pois2 else
                             ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
                              and not generic else
-                             "fused, k_gal_mid_init (160^2: one launch, half spectrum in LDS)" if mid_fused and fused_init
+                             f"fused, k_gal_mid_init ({L}^2: one launch, half spectrum in LDS)" if mid_fused and fused_init
                              else "chunked" + (", runtime-planned line FFTs" if generic else "")))},
         "roofline": roofline,
         # SURVEY.md 8(d)'s per-galaxy byte model prices the reference's op-for-op path (16 fp32 words per

@@ -1966,7 +1966,8 @@ __global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
 }
 
 // ---------------------------------------------------------------- fused Gaussian iteration at 160^2
-// k_gal_small_p's one-pass design for a runtime-planned size whose half spectrum still fits in LDS: at 160^2 the
+// k_gal_small_p's one-pass design for a runtime-planned size whose half spectrum still fits in LDS (80, 112, 144 and
+// 160: mid_size, with lines of 16 lanes x L / 16 points; the numbers below are 160^2's): at 160^2 the
 // packed row spectra PR[kx][p] take 160 x 81 complex = 101 KiB, the 32 lines' exchange areas 44 KiB, so one
 // 512-thread workgroup per galaxy runs rows -> columns + update -> inverse rows on chip (the runtime-planned
 // three-kernel chain moves ~19 words per pixel through the workspace; this moves 2 img + 5.5 half = 7.5).  Lines
@@ -1974,7 +1975,7 @@ __global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
 // back), looped over the 80 row pairs / 81 columns.  The state layout is the generic path's [N][K][L] (what
 // its init writes), the per-bin arithmetic gauss_iter_elem's, so this is a drop-in for the C_G_ITER* chain.
 #ifndef GD_MID_FUSED
-#define GD_MID_FUSED 1  // 1: 160^2 Gaussian iterations in one launch (k_gal_mid); 0: the runtime-planned chain
+#define GD_MID_FUSED 1  // 1: Gaussian iterations (and init) at the mid_size sizes in one launch (k_gal_mid); 0: the runtime-planned chains
 #endif
 template <int L, int TP, int TQ, int NT, bool FIRST, bool LAST>
 __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
@@ -3077,26 +3078,48 @@ struct Ops {
 };
 
 // the launch the runtime-planned Gaussian iteration uses at 160^2 (GOps::admm_iter_gauss)
-inline int gal_mid_launch(const Args& a, hipStream_t st) {
-    constexpr int L = 160, NT = 512;
-    static const char* names[4] = {"k_gal_mid<160,MID>", "k_gal_mid<160,FIRST>", "k_gal_mid<160,LAST>",
-                                   "k_gal_mid<160,FIRST_LAST>"};
+// the square sizes with a fused one-workgroup Gaussian iteration and init (k_gal_mid, k_gal_mid_init): L = 16 TQ,
+// lines of 16 lanes (a divisor of the wave) x TQ points (radix 5, 7, 9 = 3 x 3, 10), the packed half spectrum and
+// 32 lines' exchange areas in LDS (144^2: 126 KiB, 160^2: 147 KiB)
+inline bool mid_size(int H, int W) { return H == W && (H == 80 || H == 112 || H == 144 || H == 160); }
+template <int L>
+int gal_mid_launch_t(const Args& a, hipStream_t st) {
+    constexpr int NT = 512, TP = 16, TQ = L / 16;
+    static const std::string names[4] = {"k_gal_mid<" + std::to_string(L) + ",MID>", "k_gal_mid<" + std::to_string(L) + ",FIRST>",
+                                         "k_gal_mid<" + std::to_string(L) + ",LAST>",
+                                         "k_gal_mid<" + std::to_string(L) + ",FIRST_LAST>"};
     ProfScope ps(names[a.first + 2 * a.last], st);
     if (a.first) {
-        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, true, true>), dim3(a.N), dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, true, false>), dim3(a.N), dim3(NT), 0, st, a);
+        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, TP, TQ, NT, true, true>), dim3(a.N), dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((k_gal_mid<L, TP, TQ, NT, true, false>), dim3(a.N), dim3(NT), 0, st, a);
     } else {
-        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, false, true>), dim3(a.N), dim3(NT), 0, st, a);
-        else hipLaunchKernelGGL((k_gal_mid<L, 16, 10, NT, false, false>), dim3(a.N), dim3(NT), 0, st, a);
+        if (a.last) hipLaunchKernelGGL((k_gal_mid<L, TP, TQ, NT, false, true>), dim3(a.N), dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((k_gal_mid<L, TP, TQ, NT, false, false>), dim3(a.N), dim3(NT), 0, st, a);
     }
     return check_launch("k_gal_mid");
 }
-
-inline int gal_mid_init_launch(const Args& a, hipStream_t st) {
-    constexpr int L = 160, NT = 512;
-    ProfScope ps("k_gal_mid_init<160>", st);
-    hipLaunchKernelGGL((k_gal_mid_init<L, 16, 10, NT>), dim3(a.N), dim3(NT), 0, st, a);
+template <int L>
+int gal_mid_init_launch_t(const Args& a, hipStream_t st) {
+    constexpr int NT = 512;
+    ProfScope ps("k_gal_mid_init<" + std::to_string(L) + ">", st);
+    hipLaunchKernelGGL((k_gal_mid_init<L, 16, L / 16, NT>), dim3(a.N), dim3(NT), 0, st, a);
     return check_launch("k_gal_mid_init");
+}
+inline int gal_mid_launch(const Args& a, hipStream_t st) {
+    switch (a.gH) {
+        case 80: return gal_mid_launch_t<80>(a, st);
+        case 112: return gal_mid_launch_t<112>(a, st);
+        case 144: return gal_mid_launch_t<144>(a, st);
+        default: return gal_mid_launch_t<160>(a, st);
+    }
+}
+inline int gal_mid_init_launch(const Args& a, hipStream_t st) {
+    switch (a.gH) {
+        case 80: return gal_mid_init_launch_t<80>(a, st);
+        case 112: return gal_mid_init_launch_t<112>(a, st);
+        case 144: return gal_mid_init_launch_t<144>(a, st);
+        default: return gal_mid_init_launch_t<160>(a, st);
+    }
 }
 
 #include "gd_generic.hpp"  // GOps: the same operations for any other H x W (runtime-planned line FFTs)

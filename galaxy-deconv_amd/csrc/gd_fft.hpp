@@ -167,7 +167,9 @@ __device__ __forceinline__ c2 vtwmul(c2 v) {
 }
 
 // ---------------------------------------------------------------- in-register DFTs
-constexpr int first_factor(int n) { return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : (n % 3 == 0 ? 3 : 5)); }
+constexpr int first_factor(int n) {
+    return (n % 4 == 0 && n != 4) ? 4 : (n % 2 == 0 ? 2 : (n % 3 == 0 ? 3 : (n % 5 == 0 ? 5 : 7)));
+}
 
 template <int N, bool INV>
 struct DFT {
@@ -247,6 +249,33 @@ struct DFT<5, INV> {
         x[4] = add_mi<!INV>(a1, b1);
         x[2] = add_mi<INV>(a2, b2);
         x[3] = add_mi<!INV>(a2, b2);
+    }
+};
+
+template <bool INV>
+struct DFT<7, INV> {
+    // the symmetric form (gd_generic.hpp's odd_prime_stage): b_t = x_t + x_{7-t}, d_t = x_t - x_{7-t};
+    // forward X_q = A_q - i B_q, X_{7-q} = A_q + i B_q, A_q = x0 + sum_t c_{qt} b_t, B_q = sum_t s_{qt} d_t
+    __device__ __forceinline__ static void run(c2 (&x)[7]) {
+        constexpr float c1 = 0.623489801858733530525004884004239811f, c2k = -0.222520933956314404288902564496794759f,
+                        c3 = -0.900968867902419126236102319507445051f;
+        constexpr float s1 = 0.781831482468029808708444526674057750f, s2 = 0.974927912181823607018131682993931217f,
+                        s3 = 0.433883739117558120475768332848358754f;
+        const c2 b1 = x[1] + x[6], b2 = x[2] + x[5], b3 = x[3] + x[4];
+        const c2 d1 = x[1] - x[6], d2 = x[2] - x[5], d3 = x[3] - x[4];
+        const c2 a1 = x[0] + c1 * b1 + c2k * b2 + c3 * b3;
+        const c2 a2 = x[0] + c2k * b1 + c3 * b2 + c1 * b3;
+        const c2 a3 = x[0] + c3 * b1 + c1 * b2 + c2k * b3;
+        const c2 e1 = s1 * d1 + s2 * d2 + s3 * d3;
+        const c2 e2 = s2 * d1 - s3 * d2 - s1 * d3;
+        const c2 e3 = s3 * d1 - s1 * d2 + s2 * d3;
+        x[0] = x[0] + b1 + b2 + b3;
+        x[1] = add_mi<INV>(a1, e1);
+        x[6] = add_mi<!INV>(a1, e1);
+        x[2] = add_mi<INV>(a2, e2);
+        x[5] = add_mi<!INV>(a2, e2);
+        x[3] = add_mi<INV>(a3, e3);
+        x[4] = add_mi<!INV>(a3, e3);
     }
 };
 

@@ -737,8 +737,8 @@ struct GOps {
     }
     static int admm_init_gauss(Args a0, hipStream_t st0) {
         // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
-        // 160^2: one launch, one workgroup per galaxy (k_gal_mid_init: the same state as this chain)
-        if (GD_MID_FUSED && g_fused_init && a0.gH == 160 && a0.gW == 160 && a0.pw == 0) return gal_mid_init_launch(a0, st0);
+        // 80 / 112 / 144 / 160: one launch, one workgroup per galaxy (k_gal_mid_init: the same state as this chain)
+        if (GD_MID_FUSED && g_fused_init && mid_size(a0.gH, a0.gW) && a0.pw == 0) return gal_mid_init_launch(a0, st0);
         return chunks(a0, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::rf<RF_PSF_Y>(b, st));  // placed PSF -> slot 0, max(y,0)/alpha -> slot 1
@@ -750,9 +750,9 @@ struct GOps {
         });
     }
     static int admm_iter_gauss(Args a, hipStream_t st0) {
-        // 160^2: the whole iteration in one workgroup per galaxy (k_gal_mid; the same state layout and per-bin
+        // 80 / 112 / 144 / 160: the whole iteration in one workgroup per galaxy (k_gal_mid; the same state layout and per-bin
         // arithmetic as this chain)
-        if (GD_MID_FUSED && g_fused && a.gH == 160 && a.gW == 160) return gal_mid_launch(a, st0);
+        if (GD_MID_FUSED && g_fused && mid_size(a.gH, a.gW)) return gal_mid_launch(a, st0);
         return chunks(a, st0, [&](const Args& b, hipStream_t st) {
             GD_TRY(Lc::rf<RF_ONE>(b, st));
             if (b.first)

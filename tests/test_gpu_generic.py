@@ -311,17 +311,19 @@ def test_generic_large_images_admm_and_wiener(dev, H, W):
     assert e < TOL
 
 
+@pytest.mark.parametrize("L", [80, 112, 144, 160])
 @pytest.mark.parametrize("n", [0, 1, 2, 4])
-def test_generic_fused_160_matches_chain_and_oracle(dev, n):
-    """160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum in LDS, 16-lane x
-    10-point line transforms) and the init in one launch (k_gal_mid_init) against the runtime-planned chains
-    (gd_set_fused_iteration(0), gd_set_fused_init(0)) and the fp64-capable oracle: n = 0 is init_l2 alone (x0),
-    then first / middle / last / first-and-last iterations, ragged batch of 5."""
+def test_generic_fused_mid_matches_chain_and_oracle(dev, L, n):
+    """80^2 / 112^2 / 144^2 / 160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum
+    in LDS, 16-lane x L/16-point line transforms with radix 5, 7, 9, 10) and the init in one launch
+    (k_gal_mid_init) against the runtime-planned chains (gd_set_fused_iteration(0), gd_set_fused_init(0)) and the
+    fp64-capable oracle: n = 0 is init_l2 alone (x0), then first / middle / last / first-and-last iterations,
+    ragged batch of 5."""
     from gdeconv import _lib
     from gdeconv.synth import make_batch
     lib = _lib.load()
     N = 5
-    obs, psf, alpha, _ = make_batch(N, 160, h=48, seed=41 + n, device=dev)
+    obs, psf, alpha, _ = make_batch(N, L, h=48, seed=41 + n + L, device=dev)
     gen = torch.Generator().manual_seed(77 + n)
     rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
     rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
@@ -337,6 +339,6 @@ def test_generic_fused_160_matches_chain_and_oracle(dev, n):
     ref = O.admm_forward(obs.cpu().double(), psf.cpu().double(), alpha.cpu().double(), rho1.double(), rho2.double(),
                          "Gaussian")
     e_fc, e_f, e_c = nerr(out_f, out_c), nerr(out_f, ref), nerr(out_c, ref)
-    print(f"160^2 n={n}: fused vs chain {e_fc:.2e}, vs fp64 oracle {e_f:.2e} (chain {e_c:.2e})")
+    print(f"{L}^2 n={n}: fused vs chain {e_fc:.2e}, vs fp64 oracle {e_f:.2e} (chain {e_c:.2e})")
     assert e_fc < 5e-6
     assert e_f < TOL and e_c < TOL
