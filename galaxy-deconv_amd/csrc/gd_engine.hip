@@ -3082,9 +3082,16 @@ struct Ops {
 // lines of 16 lanes (a divisor of the wave) x TQ points (radix 5, 7, 9 = 3 x 3, 10), the packed half spectrum and
 // 32 lines' exchange areas in LDS (144^2: 126 KiB, 160^2: 147 KiB)
 inline bool mid_size(int H, int W) { return H == W && (H == 80 || H == 112 || H == 144 || H == 160); }
+// threads per workgroup: 80^2 (50 KiB of LDS) takes 256, so three galaxies share a CU (VGPRs allow three waves
+// per SIMD); the larger sizes fill the LDS with one galaxy and take 512
+#ifndef GD_MID80_THREADS
+#define GD_MID80_THREADS 256
+#endif
+template <int L>
+constexpr int mid_threads() { return L <= 80 ? GD_MID80_THREADS : 512; }
 template <int L>
 int gal_mid_launch_t(const Args& a, hipStream_t st) {
-    constexpr int NT = 512, TP = 16, TQ = L / 16;
+    constexpr int NT = mid_threads<L>(), TP = 16, TQ = L / 16;
     static const std::string names[4] = {"k_gal_mid<" + std::to_string(L) + ",MID>", "k_gal_mid<" + std::to_string(L) + ",FIRST>",
                                          "k_gal_mid<" + std::to_string(L) + ",LAST>",
                                          "k_gal_mid<" + std::to_string(L) + ",FIRST_LAST>"};
@@ -3100,7 +3107,7 @@ int gal_mid_launch_t(const Args& a, hipStream_t st) {
 }
 template <int L>
 int gal_mid_init_launch_t(const Args& a, hipStream_t st) {
-    constexpr int NT = 512;
+    constexpr int NT = mid_threads<L>();
     ProfScope ps("k_gal_mid_init<" + std::to_string(L) + ">", st);
     hipLaunchKernelGGL((k_gal_mid_init<L, 16, L / 16, NT>), dim3(a.N), dim3(NT), 0, st, a);
     return check_launch("k_gal_mid_init");

@@ -52,20 +52,20 @@ def test_graphed_forward_engine_bit_identical(dev, L, N, llh):
     assert torch.equal(g(obs2, psf2, alpha2), eager2)
 
 
-@pytest.mark.parametrize("L", [80, 160])
-def test_graphed_forward_chunked_pipeline(dev, L):
+@pytest.mark.parametrize("H,W", [(100, 100), (90, 72)])
+def test_graphed_forward_chunked_pipeline(dev, H, W):
     """A forward whose runtime-planned operations run in several Infinity-Cache chunks (chunk bytes
-    forced down to two galaxies; 4096 x 160^2 in the bench does the same at 96 MiB) captures and
-    replays bit-identically; the chunks go in sequence under capture."""
+    forced down to two galaxies; the 4096 x 160^2 bench line did the same at 96 MiB before 160^2 was fused)
+    captures and replays bit-identically; the chunks go in sequence under capture."""
     from gdeconv import _lib
     from gdeconv.graphs import GraphedForward
     from gdeconv.synth import make_batch
     lib = _lib.load()
-    tgal = 2 * (L // 2 + 1) * L * 8
+    tgal = 2 * (W // 2 + 1) * H * 8
     old = lib.gd_set_chunk_bytes(2 * tgal)
     try:
         m = _model(8, "Gaussian", dev, identity=True)
-        obs, psf, alpha, _ = make_batch(7, L, seed=11, device=dev)
+        obs, psf, alpha, _ = make_batch(7, H, W, seed=11, device=dev)
         with torch.no_grad():
             eager = m(obs, psf, alpha)
         g = GraphedForward(m, obs, psf, alpha, clone=True)
