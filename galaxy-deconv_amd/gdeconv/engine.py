@@ -95,14 +95,19 @@ def _psf(k, N, H, name="psf"):
     return k, gstride
 
 
+_WS_BYTES = {}  # (N, H, W) -> gd_workspace_bytes (pure in its arguments; one ctypes call per shape)
+
+
 def workspace(N, H, W, device):
     """Scratch of gd_workspace_bytes(N, H, W) bytes for ONE call, from torch's caching allocator on
     the current stream of ``device`` (freed back to that stream's pool when the caller drops it, so
     reuse is stream-ordered; nothing is shared across streams or threads)."""
-    lib = _lib.load()
-    if not lib.gd_supported_size(H, W):
-        raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 1638])")
-    nbytes = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
+    nbytes = _WS_BYTES.get((N, H, W))
+    if nbytes is None:
+        lib = _lib.load()
+        if not lib.gd_supported_size(H, W):
+            raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 1638])")
+        nbytes = _WS_BYTES[(N, H, W)] = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
@@ -549,9 +554,13 @@ class ADMMState:
         if llh not in _lib.GD_LLH:
             raise ValueError("llh must be 'Gaussian' or 'Poisson'")
         self.llh = _lib.GD_LLH[llh]
-        if not self.lib.gd_supported_size(self.H, self.W):
-            raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 1638])")
-        nbytes = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W, self.llh))
+        skey = (self.N, self.H, self.W, self.llh)
+        nbytes = ADMMState._state_bytes.get(skey)
+        if nbytes is None:
+            if not self.lib.gd_supported_size(self.H, self.W):
+                raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 1638])")
+            nbytes = ADMMState._state_bytes[skey] = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W,
+                                                                                      self.llh))
         with _on(self.dev):
             self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
             self.state = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
@@ -570,6 +579,7 @@ class ADMMState:
         self.init_reads_rho = r > 0
 
     _reads_rho = {}     # (H, W, llh) -> gd_admm_init_reads_rho
+    _state_bytes = {}   # (N, H, W, llh) -> gd_admm_state_bytes (pure in its arguments)
     _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (created once)
 
     @property

@@ -39,6 +39,9 @@ def pretty(kname):
     m = re.search(r"k_subnet_rhos_init<(\d+)>", kname)
     if m:
         return f"k_subnet_rhos_init<{m.group(1)}>"   # SubNet + the small-image init in one launch
+    m = re.search(r"k_gal_mid_init<(\d+),", kname)
+    if m:
+        return f"k_gal_mid_init<{m.group(1)}>"        # fused init at the mid sizes (80 / 112 / 144 / 160)
     m = re.search(r"k_gal_(?:small_t|small_p|mid)<(\d+), \d+, \d+(?:, \d+)?, (true|false), (true|false)>", kname)
     if m:  # the transposing-plan small-image iteration: same role (and names) as k_gal_small
         first, last = m.group(2) == "true", m.group(3) == "true"
@@ -131,7 +134,7 @@ def main():
     L = a.size
     if a.iters is None:  # forwards in the run = launches of the one-per-forward init kernel
         fw = 0
-        for k in (f"k_gal_init<{L},REG>", f"k_gal_init<{L},POIS>", f"k_gal_small_init<{L}>",
+        for k in (f"k_gal_init<{L},REG>", f"k_gal_init<{L},POIS>", f"k_gal_small_init<{L}>", f"k_gal_mid_init<{L}>",
                   f"k_subnet_rhos_init<{L}>", f"k_gal_init<{L},ONE>", f"k_gal_init<{L},W1>"):
             fw = fw or out["kernels"].get(k, {}).get("launches", 0)
         a.iters = fw * (a.n_iters or 8) if fw else 24
@@ -172,6 +175,8 @@ def main():
         init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},REG>"]
     if f"k_gal_small_init<{L}>" in out["kernels"]:
         init = [f"k_gal_small_init<{L}>"]
+    if f"k_gal_mid_init<{L}>" in out["kernels"]:
+        init = [f"k_gal_mid_init<{L}>"]
     if all(k in out["kernels"] for k in init):
         out["kernels"][f"op_admm_init<{L},Gaussian>"] = {
             "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in init),
