@@ -2060,6 +2060,299 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
         }
     }
 }
+// ---------------------------------------------------------------- fused Poisson iteration, L <= 112
+// The reference's default llh (models/Unrolled_ADMM.py:154): the V step's sqrt keeps u1 and w = v - u2 in the
+// image domain, so an iteration transforms TWO images (z - u1 and w) and inverts two spectra (X and H X).  At
+// L <= 112 both images' packed row spectra fit in LDS (2 L (L/2 + 1) complex: 100 KiB at 112^2), so the
+// three-kernel chain RF_ITER -> C_ITER -> RI_ITER (two workspace round trips per iteration) becomes one
+// workgroup per galaxy, on k_gal_mid's layout and lines (TP lanes x TQ points):
+//   R  row pairs of z - u1 (image 0) and of w (image 1) -> FFT -> packed spectra PR[im][kx][p]
+//   C  per column kx: both images' columns (separated from the packed columns kx, L - kx), FFT; C_ITER's
+//      X = (rho1 F(z - u1) + rho2 conj(H) F(w)) / (rho1 |H|^2 + rho2) and H X (IEEE divisions, as the chain);
+//      IFFT both; the packed inputs of the inverse rows written in place
+//   I  row pairs: IFFT -> x, H x -> RI_ITER's pointwise update (u1, w, zin; x alpha on the last iteration)
+// State: the OTF [N][K][L] (C_OTF_INIT's, not re-read by the row phases), u1, w (images); reads z, u1, w, y, the
+// OTF; writes u1, w, zin: 6 img + 1 half per galaxy against 10 img + 7 half for the chain.
+template <int L, int TP, int TQ, int NT, bool LAST>
+__global__ __launch_bounds__(NT) void k_pois_small(Args a) {
+    constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1, IMS = L * SP;
+    constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    static_assert(TP * TQ == L && TP >= TQ && TP % 2 == 0 && NT % G == 0 && 64 % TP == 0, "lines of TP lanes in one wave");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 PR[2 * IMS];
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, NT);
+    const float r1 = a.rho1(g), r2 = a.rho2(g), al = a.alpha(g), r2n = LAST ? 1.f : a.rho2n(g);
+    const size_t gi = (size_t)g * L * L;
+    const float* z = a.a0 + gi;
+    const float* u1 = a.a1 + gi;
+    const float* wv = a.a2 + gi;
+    __syncthreads();
+    float2 v[G], q[G];
+
+    // R: job t < L/2: pair t of z - u1; job t >= L/2: pair t - L/2 of w
+    for (int t = line; t < L; t += LINES) {
+        const int im = t >= L / 2, p = t - im * (L / 2), o0 = (2 * p) * L + j, o1 = o0 + L;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s)
+            v[s] = im ? make_float2(wv[o0 + TP * s], wv[o1 + TP * s])
+                      : make_float2(z[o0 + TP * s] - u1[o0 + TP * s], z[o1 + TP * s] - u1[o1 + TP * s]);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[im * IMS + (j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();
+
+    // C
+    const bool odd = j & 1, cl = j < TQ;
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[kx * SP + p], Dm = PR[km * SP + p];
+            const float2 E = PR[IMS + kx * SP + p], Fm = PR[IMS + km * SP + p];
+            v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+            q[s] = odd ? make_float2(0.5f * (E.y + Fm.y), 0.5f * (Fm.x - E.x)) : make_float2(0.5f * (E.x + Fm.x), 0.5f * (E.y - Fm.y));
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        tline_fft<L, TP, TQ, false>(q, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) {
+            const float2 Hk = a.otf[ob + TQ * k1];
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;  // C_ITER's arithmetic
+            const float lhs = r1 * HtH + r2;
+            const float2 HtW = cmulc(q[k1], Hk);
+            const float2 rhs = make_float2(r1 * v[k1].x + r2 * HtW.x, r1 * v[k1].y + r2 * HtW.y);
+            const float2 X = make_float2(rhs.x / lhs, rhs.y / lhs);
+            v[k1] = cscale(X, inv_n);
+            q[k1] = cscale(cmul(Hk, X), inv_n);
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        tline_fft<L, TQ, TP, true>(q, j, my, tw);
+        const bool self = (kx == 0) || (2 * kx == L);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {  // both images' packed inverse-row inputs (k_gal_mid's write-back)
+            const int p = (j >> 1) + (TP / 2) * s;
+#pragma unroll
+            for (int im = 0; im < 2; ++im) {
+                const float2 c = im ? q[s] : v[s];
+                const float ox = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.x), 0xB1, 0xF, 0xF, false));
+                const float oy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c.y), 0xB1, 0xF, 0xF, false));
+                float2 be = odd ? make_float2(ox, oy) : c, bo = odd ? c : make_float2(ox, oy);
+                if (odd) {
+                    be = cconj(be);
+                    bo = cconj(bo);
+                }
+                if (self) {
+                    be.y = 0.f;
+                    bo.y = 0.f;
+                }
+                if (!(odd && self)) PR[im * IMS + (odd ? km : kx) * SP + p] = make_float2(be.x - bo.y, be.y + bo.x);
+            }
+        }
+    }
+    __syncthreads();
+
+    // I: x (image 0), H x (image 1) -> RI_ITER (models/Unrolled_ADMM.py:207-215)
+    for (int p = line; p < L / 2; p += LINES) {
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) {
+                v[k1] = PR[(j + TQ * k1) * SP + p];
+                q[k1] = PR[IMS + (j + TQ * k1) * SP + p];
+            }
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        tline_fft<L, TQ, TP, true>(q, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const size_t pix = gi + (size_t)(2 * p + h) * L + j + TP * s;
+                const float x = h ? v[s].y : v[s].x, hx = h ? q[s].y : q[s].x;
+                if (LAST) {
+                    a.o2[pix] = x * al;  // Poisson: x_list[-1] * alpha (:215)
+                } else {
+                    const float un = (a.a1[pix] + x) - a.a0[pix];        // u1 + x - z
+                    const float u2 = hx - a.a2[pix];                     // u2 + conv(H, x) - v  (w = v - u2)
+                    const float vn = v_step(GD_LLH_POISSON, hx + u2, fmaxf(a.y[pix], 0.f), r2n, al);
+                    a.o0[pix] = un;
+                    a.o1[pix] = vn - u2;
+                    a.o2[pix] = x + un;                                  // next denoiser input
+                }
+            }
+        }
+    }
+}
+
+// The Poisson init at L <= 112 in one launch (k_pois_small_init): init_l2 (models/Unrolled_ADMM.py:170-175) and
+// the first V step (:207) on k_pois_small's layout - the chain RF_PSF_Y -> C_OTF_INIT -> RIF_CLAMP -> C_CONV ->
+// RI_INIT, bin for bin and pixel for pixel:
+//   R  row pairs of the placed PSF (psf_to_otf's circular placement) and of max(y, 0) / alpha -> PR[0], PR[1]
+//   C  per column: both FFT'd; the OTF -> state; X0 = conj(H) Y / (|H|^2 + 1/alpha) / L^2; IFFT -> PR[1]
+//   I  x0 = clamp(IFFT, 0, 1) -> zin; FFT -> PR[1]
+//   C  per column: F(x0) H / L^2 (the OTF column read back); IFFT -> PR[1]
+//   I  H x0 -> w1 = V(H x0 + 0, y, rho2, alpha) (u2 = 0: w = v), u1 = 0
+template <int L, int TP, int TQ, int NT>
+__global__ __launch_bounds__(NT) void k_pois_small_init(Args a) {
+    constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1, IMS = L * SP;
+    constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    static_assert(TP * TQ == L && TP >= TQ && TP % 2 == 0 && NT % G == 0 && 64 % TP == 0, "lines of TP lanes in one wave");
+    constexpr float inv_n = float(1.0 / double(L * L));
+    __shared__ float2 tw[L];
+    __shared__ float2 PR[2 * IMS];
+    __shared__ float2 xch[LINES * XCH];
+    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
+    const int g = blockIdx.x;
+    float2* my = xch + line * XCH;
+    fill_twiddles<L>(tw, tid, NT);
+    const float al = a.alpha(g), r2 = a.rho2n(g);
+    const int h = a.h, h2 = h >> 1;
+    const float* psf = a.psf + (long long)g * a.psf_gstride;
+    const size_t gi = (size_t)g * L * L;
+    const float* y = a.y + gi;
+    __syncthreads();
+    float2 v[G], q[G];
+    const bool odd = j & 1, cl = j < TQ;
+    // the packed row-pair spectra of image im -> column kx's bins (lane j: rows j + TP s)
+    auto separate = [&](float2 (&c)[G], int im, int kx, int km) {
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float2 C = PR[im * IMS + kx * SP + p], Dm = PR[im * IMS + km * SP + p];
+            c[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
+        }
+    };
+    // column results (transposed back) -> the packed inputs of the inverse rows of image im, in place
+    auto pack_back = [&](const float2 (&c)[G], int im, int kx, int km) {
+        const bool self = (kx == 0) || (2 * kx == L);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            const int p = (j >> 1) + (TP / 2) * s;
+            const float ox = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c[s].x), 0xB1, 0xF, 0xF, false));
+            const float oy = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(c[s].y), 0xB1, 0xF, 0xF, false));
+            float2 be = odd ? make_float2(ox, oy) : c[s], bo = odd ? c[s] : make_float2(ox, oy);
+            if (odd) {
+                be = cconj(be);
+                bo = cconj(bo);
+            }
+            if (self) {
+                be.y = 0.f;
+                bo.y = 0.f;
+            }
+            if (!(odd && self)) PR[im * IMS + (odd ? km : kx) * SP + p] = make_float2(be.x - bo.y, be.y + bo.x);
+        }
+    };
+    // R: job t < L/2: padded PSF row pair t; t >= L/2: row pair t - L/2 of max(y, 0) / alpha (RF_PSF_Y)
+    for (int t = line; t < L; t += LINES) {
+        const int im = t >= L / 2, p = t - im * (L / 2);
+        if (im) {
+#pragma unroll
+            for (int s = 0; s < TQ; ++s) {
+                const int o = (2 * p) * L + j + TP * s;
+                v[s] = make_float2(fmaxf(y[o], 0.f) / al, fmaxf(y[o + L], 0.f) / al);
+            }
+        } else {
+            int i0 = 2 * p + h2, i1 = i0 + 1;  // padded rows 2p, 2p + 1 -> PSF rows (r + h/2) mod L (gpsf)
+            if (i0 >= L) i0 -= L;
+            if (i1 >= L) i1 -= L;
+#pragma unroll
+            for (int s = 0; s < TQ; ++s) {
+                int jj = j + TP * s + h2;
+                if (jj >= L) jj -= L;
+                const bool in = jj < h;
+                v[s] = make_float2((in && i0 < h) ? psf[i0 * h + jj] : 0.f, (in && i1 < h) ? psf[i1 * h + jj] : 0.f);
+            }
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[im * IMS + (j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();
+    // C: the OTF and X0 (C_OTF_INIT)
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+        separate(v, 0, kx, km);
+        separate(q, 1, kx, km);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        tline_fft<L, TP, TQ, false>(q, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) {
+            const float2 Hk = v[k1];
+            if (cl) a.otf[ob + TQ * k1] = Hk;
+            const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;
+            const float lhs = HtH + 1.0f / al;
+            const float2 rhs = cmulc(q[k1], Hk);
+            q[k1] = cscale(make_float2(rhs.x / lhs, rhs.y / lhs), inv_n);
+        }
+        tline_fft<L, TQ, TP, true>(q, j, my, tw);
+        pack_back(q, 1, kx, km);
+    }
+    __syncthreads();
+    // I: x0 = clamp -> zin (RIF_CLAMP); FFT of x0's rows
+    float* zin = a.o2 + gi;
+    for (int p = line; p < L / 2; p += LINES) {
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) v[k1] = PR[IMS + (j + TQ * k1) * SP + p];
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            v[s] = make_float2(fminf(fmaxf(v[s].x, 0.f), 1.f), fminf(fmaxf(v[s].y, 0.f), 1.f));
+            zin[(2 * p) * L + j + TP * s] = v[s].x;
+            zin[(2 * p + 1) * L + j + TP * s] = v[s].y;
+        }
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) PR[IMS + (j + TQ * k1) * SP + p] = v[k1];
+        }
+    }
+    __syncthreads();
+    // C: conv(H, x0) (C_CONV)
+    for (int kx = line; kx < K; kx += LINES) {
+        const int km = kx == 0 ? 0 : L - kx;
+        separate(v, 1, kx, km);
+        tline_fft<L, TP, TQ, false>(v, j, my, tw);
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) v[k1] = cscale(cmul(v[k1], a.otf[ob + TQ * k1]), inv_n);
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+        pack_back(v, 1, kx, km);
+    }
+    __syncthreads();
+    // I: w1 = V(H x0 + 0, y, rho2, alpha), u1 = 0 (RI_INIT)
+    for (int p = line; p < L / 2; p += LINES) {
+        if (j < TQ) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) v[k1] = PR[IMS + (j + TQ * k1) * SP + p];
+        }
+        tline_fft<L, TQ, TP, true>(v, j, my, tw);
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const size_t pix = gi + (size_t)(2 * p + hh) * L + j + TP * s;
+                const float hx = hh ? v[s].y : v[s].x;
+                a.o1[pix] = v_step(GD_LLH_POISSON, hx + 0.0f, fmaxf(a.y[pix], 0.f), r2, al);
+                a.o0[pix] = 0.f;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- fused Gaussian init at 160^2
 // init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants and F(x0) in one launch, one 512-thread
 // workgroup per galaxy on k_gal_mid's layout: the runtime-planned chain RF_PSF_Y -> C_G_INIT -> RIF_CLAMP ->
@@ -2901,6 +3194,37 @@ int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
     return for_chunks_hw(a, L, L, st, std::forward<F>(f));
 }
 
+// k_pois_small's line plans (TP lanes x TQ points, threads).  Not at 128^2: there both images fill 152 KiB of LDS,
+// one 256-thread workgroup per CU, and the chain's kernels were faster (4096 galaxies: 1.33 vs 0.95 ms per
+// iteration; profiles/r04pois_*); at 64^2 / 96^2 / 112^2 the fused form takes 0.82 / 0.95 / 0.46 of the chain's time
+template <int L>
+struct PoisSmallPlan;
+template <> struct PoisSmallPlan<32> { static constexpr int TP = 8, TQ = 4, NT = 256; };
+template <> struct PoisSmallPlan<48> { static constexpr int TP = 8, TQ = 6, NT = 256; };
+template <> struct PoisSmallPlan<64> { static constexpr int TP = 8, TQ = 8, NT = 256; };
+template <> struct PoisSmallPlan<80> { static constexpr int TP = 16, TQ = 5, NT = 256; };
+template <> struct PoisSmallPlan<96> { static constexpr int TP = 16, TQ = 6, NT = 512; };
+template <> struct PoisSmallPlan<112> { static constexpr int TP = 16, TQ = 7, NT = 512; };
+#ifndef GD_POIS_SMALL
+#define GD_POIS_SMALL 1  // 1: Poisson iterations at L <= 112 in one launch (k_pois_small); 0: the three-kernel chain
+#endif
+template <int L>
+int pois_small_init_launch(const Args& a, hipStream_t st) {
+    using PL = PoisSmallPlan<L>;
+    ProfScope ps("k_pois_small_init<" + std::to_string(L) + ">", st);
+    hipLaunchKernelGGL((k_pois_small_init<L, PL::TP, PL::TQ, PL::NT>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    return check_launch("k_pois_small_init");
+}
+template <int L>
+int pois_small_launch(const Args& a, hipStream_t st) {
+    using PL = PoisSmallPlan<L>;
+    static const std::string names[2] = {"k_pois_small<" + std::to_string(L) + ",MID>", "k_pois_small<" + std::to_string(L) + ",LAST>"};
+    ProfScope ps(names[a.last ? 1 : 0], st);
+    if (a.last) hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    else hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, false>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    return check_launch("k_pois_small");
+}
+
 // Operation bodies, templated on L.
 template <int L>
 struct Ops {
@@ -2953,6 +3277,9 @@ struct Ops {
     }
     static int admm_init(Args a0, hipStream_t st0) {
         // Poisson: a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
+        if constexpr (L <= 112) {
+            if (GD_POIS_SMALL && g_fused_init) return pois_small_init_launch<L>(a0, st0);  // one launch
+        }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::template rf<RF_PSF_Y>(b, st));
@@ -3009,6 +3336,9 @@ struct Ops {
     }
     static int admm_iter(Args a0, hipStream_t st0) {
         // Poisson: a.a0 = z, a.a1 = u1 (RF reads), a.a2 = w; RI: a.o0 = u1, a.o1 = w, a.o2 = zin / out
+        if constexpr (L <= 112) {
+            if (GD_POIS_SMALL && g_fused) return pois_small_launch<L>(a0, st0);  // one workgroup per galaxy
+        }
         return for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::template rf<RF_ITER>(a, st));
             GD_TRY(Lc::template col<C_ITER>(a, st));

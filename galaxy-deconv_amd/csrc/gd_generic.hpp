@@ -724,7 +724,9 @@ struct GOps {
         return Lc::ri<RI_OUT1>(a, st);
     }
     static int admm_init(Args a0, hipStream_t st0) {
-        // Poisson: a.o0 = u1, a.o1 = w, a.o2 = zin (x0)
+        // Poisson: a.o0 = u1, a.o1 = w, a.o2 = zin (x0); 80^2 / 112^2 in one launch (k_pois_small_init)
+        if (GD_POIS_SMALL && g_fused_init && a0.gH == a0.gW && (a0.gH == 80 || a0.gH == 112) && a0.pw == 0)
+            return a0.gH == 80 ? pois_small_init_launch<80>(a0, st0) : pois_small_init_launch<112>(a0, st0);
         return chunks(a0, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::rf<RF_PSF_Y>(b, st));
@@ -763,6 +765,9 @@ struct GOps {
         });
     }
     static int admm_iter(Args a0, hipStream_t st0) {
+        // Poisson at 80^2 / 112^2: one workgroup per galaxy (k_pois_small: the same state as this chain)
+        if (GD_POIS_SMALL && g_fused && a0.gH == a0.gW && (a0.gH == 80 || a0.gH == 112))
+            return a0.gH == 80 ? pois_small_launch<80>(a0, st0) : pois_small_launch<112>(a0, st0);
         return chunks(a0, st0, [&](const Args& a, hipStream_t st) {
             GD_TRY(Lc::rf<RF_ITER>(a, st));
             GD_TRY(Lc::col<C_ITER>(a, st));

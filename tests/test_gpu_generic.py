@@ -311,6 +311,38 @@ def test_generic_large_images_admm_and_wiener(dev, H, W):
     assert e < TOL
 
 
+@pytest.mark.parametrize("L", [32, 48, 64, 80, 96, 112])
+@pytest.mark.parametrize("n", [0, 1, 3])
+def test_fused_poisson_small_matches_chain_and_oracle(dev, L, n):
+    """Poisson (the reference's default llh) at L <= 112: the init (k_pois_small_init: init_l2 and the first V
+    step) and each iteration (k_pois_small) in one launch, both images' packed row spectra in LDS, against the
+    chains (gd_set_fused_iteration(0), gd_set_fused_init(0)) and the fp64 oracle: x0 alone (n = 0), last-only
+    (n = 1) and middle + last iterations, ragged batch of 5."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N = 5
+    obs, psf, alpha, _ = make_batch(N, L, h=min(48, L // 2 * 2 - 16 if L < 64 else 48), seed=61 + n + L, device=dev)
+    gen = torch.Generator().manual_seed(91 + n + L)
+    rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
+    rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).float()
+    m = _spectral_model(n, "Poisson", dev, rho1, rho2)
+    with torch.no_grad():
+        out_f = m(obs, psf, alpha).cpu()
+        old, old_i = lib.gd_set_fused_iteration(0), lib.gd_set_fused_init(0)
+        try:
+            out_c = m(obs, psf, alpha).cpu()
+        finally:
+            lib.gd_set_fused_iteration(old)
+            lib.gd_set_fused_init(old_i)
+    ref = O.admm_forward(obs.cpu().double(), psf.cpu().double(), alpha.cpu().double(), rho1.double(), rho2.double(),
+                         "Poisson")
+    e_fc, e_f, e_c = nerr(out_f, out_c), nerr(out_f, ref), nerr(out_c, ref)
+    print(f"Poisson {L}^2 n={n}: fused vs chain {e_fc:.2e}, vs fp64 oracle {e_f:.2e} (chain {e_c:.2e})")
+    assert e_fc < 5e-6
+    assert e_f < TOL
+
+
 @pytest.mark.parametrize("L", [80, 112, 144, 160])
 @pytest.mark.parametrize("n", [0, 1, 2, 4])
 def test_generic_fused_mid_matches_chain_and_oracle(dev, L, n):
