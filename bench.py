@@ -129,6 +129,10 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
                 return 2 * img + 2 * half
             mid, first, last = 5 * img + 7 * half, 5 * img + 6 * half, 2 * img + 3 * half
             return (first + mid * (n - 2) + last) / n
+        if fused and L <= 112:
+            # k_pois_small: z, u1, w, y and the OTF in; u1, w, zin out (last: z, u1, w, OTF in, x alpha out)
+            mid, last = 7 * img + half, 4 * img + half
+            return (mid * (n - 1) + last) / n
         # u1, w (= v - u2), z in; u1, w, zin out (+ y, the OTF half spectrum); the last iteration
         # reads z, u1, w, y, OTF and writes x only
         mid, last = 6 * img + 2 * half, 4 * img + half
@@ -171,15 +175,15 @@ def kernel_bytes(name, L, n_iters):
     return table.get(k)
 
 
-def graph_iter_ms(obs, psf, alpha, dev, reps=64):
-    """Average device time of one middle Gaussian ADMM iteration (gd_admm_iter) without host gaps: ``reps``
-    launches on one state, z fixed, captured in a hipGraph and replayed between two HIP events."""
+def graph_iter_ms(obs, psf, alpha, dev, reps=64, llh="Gaussian"):
+    """Average device time of one middle ADMM iteration (gd_admm_iter) without host gaps: ``reps`` launches on
+    one state, z fixed, captured in a hipGraph and replayed between two HIP events."""
     from gdeconv import engine
     N = obs.shape[0]
     with torch.no_grad():
-        st = engine.ADMMState(obs, psf, alpha, "Gaussian")
-        st.init(None)
+        st = engine.ADMMState(obs, psf, alpha, llh)
         r = engine.RhoSchedule(torch.ones(N, 1, 1, reps + 2, device=dev), N, dev)
+        st.init(r[0] if st.init_reads_rho else None)
         z = st.zin.clone()
         st.step(z, r[0], r[0], r[1])  # iteration 0 (FIRST) outside the graph
         side = torch.cuda.Stream()
@@ -392,6 +396,8 @@ def main():
     mid_fused = bool(fused) and args.size in (80, 112, 144, 160) and args.llh == "Gaussian"
     use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian"
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
+    # Poisson at L <= 112: one workgroup per galaxy, both images in LDS (k_pois_small, k_pois_small_init)
+    pois_small = bool(fused) and args.llh == "Poisson" and args.size in (32, 48, 64, 80, 96, 112)
     if args.pipe_streams is not None:
         lib.gd_set_pipeline_streams(args.pipe_streams)
     pipe_streams = lib.gd_set_pipeline_streams(0)
@@ -558,30 +564,30 @@ def main():
     kern = {k: v for k, v in kstats.items() if not k.startswith("op_")}
     pipelined = chunk_bytes > 0
     h_psf = psf.shape[-1]
-    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused or pois2, h_psf)}
+    priced_ops = {k: v for k, v in ops.items() if op_bytes(k, L, n, use_fused or pois2 or pois_small, h_psf)}
     # every priced operation against the HBM spec (compulsory bytes / average call time)
     for k, (ms, c) in ops.items():
-        b = op_bytes(k, L, n, use_fused or pois2, h_psf)
+        b = op_bytes(k, L, n, use_fused or pois2 or pois_small, h_psf)
         if b:
             ach = b * N / (ms / c * 1e-3) / 1e9
             kernels[pretty(k)].update({"algorithmic_bytes_per_call": b * N, "achieved_GBs": ach,
                                        "frac_of_hbm_peak": ach / HBM_PEAK_GBS})
-    if (pipelined or use_fused or pois2) and priced_ops:
+    if (pipelined or use_fused or pois2 or pois_small) and priced_ops:
         # chunks of RF -> C -> RI run concurrently on several streams: the roofline unit is the
         # whole ADMM iteration (one op_admm_iter call), timed on the caller's stream
         dom_raw = max(priced_ops, key=lambda k: ops[k][0])
         dom_ms = ops[dom_raw][0] / ops[dom_raw][1]
-        per_gal = op_bytes(dom_raw, L, n, use_fused or pois2, h_psf)
+        per_gal = op_bytes(dom_raw, L, n, use_fused or pois2 or pois_small, h_psf)
     else:
         priced = {k: v for k, v in kern.items() if kernel_bytes(k, L, n)} or kern
         dom_raw = max(priced, key=lambda k: kern[k][0])
         dom_ms = kern[dom_raw][0] / kern[dom_raw][1]
         per_gal = kernel_bytes(dom_raw, L, n)
     timing = "HIP events on the caller's stream around each call, profiling pass"
-    if (use_fused and not rl and dom_ms < 0.05 and pretty(dom_raw) == f"op_admm_iter<{L},Gaussian>"):
+    if (not rl and dom_ms < 0.05 and pretty(dom_raw) == f"op_admm_iter<{L},{args.llh}>"):
         # a short op of a host-bound eager forward (48^2): the events also time the host's enqueue gaps, so
         # the launch duration comes from back-to-back launches replayed as one hipGraph instead
-        dom_ms = graph_iter_ms(obs, psf, alpha, dev)
+        dom_ms = graph_iter_ms(obs, psf, alpha, dev, llh=args.llh)
         timing = "64 back-to-back middle iterations (gd_admm_iter) replayed as one hipGraph, HIP events around it"
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
@@ -639,6 +645,8 @@ def main():
                                  if use_fused else (rl_impl if rl else
                                                     ("two whole-galaxy passes: k_gal_reg<POIS> (X update, u1, zin) + "
                                                      "k_pois_b (Hx, V step, duals, conj(H) F(w))") if pois2
+                                                    else (f"fused, k_pois_small ({L}^2: both images in LDS, one workgroup "
+                                                          "per galaxy)") if pois_small
                                                     else "three-kernel, runtime-planned line FFTs (gd_generic.hpp)"
                                                     if generic else "three-kernel")),
                    "init": (None if rl else
@@ -649,6 +657,8 @@ def main():
                             ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
                              and not generic else
                              f"fused, k_gal_mid_init ({L}^2: one launch, half spectrum in LDS)" if mid_fused and fused_init
+                             else f"fused, k_pois_small_init ({L}^2: one launch, both images in LDS)"
+                             if pois_small and fused_init
                              else "chunked" + (", runtime-planned line FFTs" if generic else "")))},
         "roofline": roofline,
         # SURVEY.md 8(d)'s per-galaxy byte model prices the reference's op-for-op path (16 fp32 words per
