@@ -311,6 +311,35 @@ def test_generic_large_images_admm_and_wiener(dev, H, W):
     assert e < TOL
 
 
+@pytest.mark.parametrize("L,llh", [(48, "Poisson"), (80, "Poisson"), (80, "Gaussian"), (144, "Gaussian")])
+def test_fused_one_workgroup_kernels_shared_psf_and_scalar_alpha(dev, L, llh):
+    """The fused one-workgroup kernels (k_pois_small*, k_gal_mid*) with ONE PSF for the whole batch (psf batch 1:
+    galaxy stride 0) and a Python-number alpha (stride 0), against the chains and the fp64 oracle."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    N, n = 3, 2
+    obs, psf, alpha, _ = make_batch(N, L, h=32, seed=7 + L, device=dev)
+    psf1 = psf[:1].contiguous()
+    rho1 = torch.tensor([0.8, 1.3]).float()
+    rho2 = torch.tensor([1.1, 0.6]).float()
+    m = _spectral_model(n, llh, dev, rho1.to(dev), rho2.to(dev))
+    with torch.no_grad():
+        out_f = m(obs, psf1, 0.7).cpu()
+        old, old_i = lib.gd_set_fused_iteration(0), lib.gd_set_fused_init(0)
+        try:
+            out_c = m(obs, psf1, 0.7).cpu()
+        finally:
+            lib.gd_set_fused_iteration(old)
+            lib.gd_set_fused_init(old_i)
+    a64 = torch.full((N, 1, 1, 1), 0.7, dtype=torch.float64)
+    ref = O.admm_forward(obs.cpu().double(), psf1.cpu().double().expand(N, 1, 32, 32), a64,
+                         rho1.double().view(1, 1, 1, n).expand(N, 1, 1, n), rho2.double().view(1, 1, 1, n).expand(N, 1, 1, n), llh)
+    e_fc, e_f = nerr(out_f, out_c), nerr(out_f, ref)
+    print(f"{llh} {L}^2 shared PSF, scalar alpha: fused vs chain {e_fc:.2e}, vs fp64 oracle {e_f:.2e}")
+    assert e_fc < 5e-6 and e_f < TOL
+
+
 @pytest.mark.parametrize("L", [32, 48, 64, 80, 96, 112])
 @pytest.mark.parametrize("n", [0, 1, 3])
 def test_fused_poisson_small_matches_chain_and_oracle(dev, L, n):
