@@ -2073,7 +2073,9 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
 //   I  row pairs: IFFT -> x, H x -> RI_ITER's pointwise update (u1, w, zin; x alpha on the last iteration)
 // State: the OTF [N][K][L] (C_OTF_INIT's, not re-read by the row phases), u1, w (images); reads z, u1, w, y, the
 // OTF; writes u1, w, zin: 6 img + 1 half per galaxy against 10 img + 7 half for the chain.
-template <int L, int TP, int TQ, int NT, bool LAST>
+// FIRST (state layout 4, after a SPLIT init): the w slot holds H x0; the row phase forms w1 = V(H x0 + 0, y, rho2,
+// alpha) there (RI_INIT's arithmetic with this iteration's rho2, the init's rho2_iters[0]) and stores it back
+template <int L, int TP, int TQ, int NT, bool LAST, bool FIRST = false>
 __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
     constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1, IMS = L * SP;
     constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
@@ -2098,9 +2100,19 @@ __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
     for (int t = line; t < L; t += LINES) {
         const int im = t >= L / 2, p = t - im * (L / 2), o0 = (2 * p) * L + j, o1 = o0 + L;
 #pragma unroll
-        for (int s = 0; s < TQ; ++s)
-            v[s] = im ? make_float2(wv[o0 + TP * s], wv[o1 + TP * s])
-                      : make_float2(z[o0 + TP * s] - u1[o0 + TP * s], z[o1 + TP * s] - u1[o1 + TP * s]);
+        for (int s = 0; s < TQ; ++s) {
+            if (FIRST && im) {  // w1 from H x0 (the SPLIT init), stored for the update phase
+                const size_t p0 = gi + o0 + TP * s, p1 = gi + o1 + TP * s;
+                const float w0 = v_step(GD_LLH_POISSON, wv[o0 + TP * s] + 0.0f, fmaxf(a.y[p0], 0.f), r2, al);
+                const float w1 = v_step(GD_LLH_POISSON, wv[o1 + TP * s] + 0.0f, fmaxf(a.y[p1], 0.f), r2, al);
+                a.o1[p0] = w0;
+                a.o1[p1] = w1;
+                v[s] = make_float2(w0, w1);
+            } else {
+                v[s] = im ? make_float2(wv[o0 + TP * s], wv[o1 + TP * s])
+                          : make_float2(z[o0 + TP * s] - u1[o0 + TP * s], z[o1 + TP * s] - u1[o1 + TP * s]);
+            }
+        }
         tline_fft<L, TP, TQ, false>(v, j, my, tw);
         if (j < TQ) {
 #pragma unroll
@@ -2201,20 +2213,29 @@ __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
 //   I  x0 = clamp(IFFT, 0, 1) -> zin; FFT -> PR[1]
 //   C  per column: F(x0) H / L^2 (the OTF column read back); IFFT -> PR[1]
 //   I  H x0 -> w1 = V(H x0 + 0, y, rho2, alpha) (u2 = 0: w = v), u1 = 0
+// SPLIT (the state layout gd_admm_state_layout 4): the last step stores H x0 itself in the w slot and reads no
+// rho; iteration 0 (k_pois_small<FIRST>) forms w1 from it with its own rho2 (= the init's rho2_iters[0]), so the
+// init runs beside the SubNet (k_subnet_rhos_init) like the Gaussian one.  Same w1 bits either way.
 template <int L, int TP, int TQ, int NT>
-__global__ __launch_bounds__(NT) void k_pois_small_init(Args a) {
+struct PoisInitLds {
+    static constexpr int SP = L / 2 + 1, IMS = L * SP, LINES = NT / TP;
+    static constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    static constexpr int TW = 0, PR = L, XC = PR + 2 * IMS, SIZE = XC + LINES * XCH;  // float2 units
+};
+template <int L, int TP, int TQ, int NT, bool SPLIT>
+__device__ __forceinline__ void pois_small_init_body(const Args& a, int g, int tid, float2* lds) {
     constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1, IMS = L * SP;
-    constexpr int XCH = TP * (TQ + 1) > TQ * (TP + 1) ? TP * (TQ + 1) : TQ * (TP + 1);
+    using LY = PoisInitLds<L, TP, TQ, NT>;
+    constexpr int XCH = LY::XCH;
     static_assert(TP * TQ == L && TP >= TQ && TP % 2 == 0 && NT % G == 0 && 64 % TP == 0, "lines of TP lanes in one wave");
     constexpr float inv_n = float(1.0 / double(L * L));
-    __shared__ float2 tw[L];
-    __shared__ float2 PR[2 * IMS];
-    __shared__ float2 xch[LINES * XCH];
-    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
-    const int g = blockIdx.x;
+    float2* tw = lds + LY::TW;
+    float2* PR = lds + LY::PR;
+    float2* xch = lds + LY::XC;
+    const int line = tid / G, j = tid - line * G;
     float2* my = xch + line * XCH;
     fill_twiddles<L>(tw, tid, NT);
-    const float al = a.alpha(g), r2 = a.rho2n(g);
+    const float al = a.alpha(g), r2 = SPLIT ? 1.f : a.rho2n(g);
     const int h = a.h, h2 = h >> 1;
     const float* psf = a.psf + (long long)g * a.psf_gstride;
     const size_t gi = (size_t)g * L * L;
@@ -2346,12 +2367,28 @@ __global__ __launch_bounds__(NT) void k_pois_small_init(Args a) {
             for (int hh = 0; hh < 2; ++hh) {
                 const size_t pix = gi + (size_t)(2 * p + hh) * L + j + TP * s;
                 const float hx = hh ? v[s].y : v[s].x;
-                a.o1[pix] = v_step(GD_LLH_POISSON, hx + 0.0f, fmaxf(a.y[pix], 0.f), r2, al);
+                a.o1[pix] = SPLIT ? hx : v_step(GD_LLH_POISSON, hx + 0.0f, fmaxf(a.y[pix], 0.f), r2, al);
                 a.o0[pix] = 0.f;
             }
         }
     }
 }
+template <int L, int TP, int TQ, int NT, bool SPLIT>
+__global__ __launch_bounds__(NT) void k_pois_small_init(Args a) {
+    __shared__ __attribute__((aligned(16))) float2 lds[PoisInitLds<L, TP, TQ, NT>::SIZE];
+    pois_small_init_body<L, TP, TQ, NT, SPLIT>(a, blockIdx.x, threadIdx.x, lds);
+}
+// k_pois_small's line plans (TP lanes x TQ points, threads).  Not at 128^2: there both images fill 152 KiB of LDS,
+// one 256-thread workgroup per CU, and the chain's kernels were faster (4096 galaxies: 1.33 vs 0.95 ms per
+// iteration; profiles/r04pois_*); at 64^2 / 96^2 / 112^2 the fused form takes 0.82 / 0.95 / 0.46 of the chain's time
+template <int L>
+struct PoisSmallPlan;
+template <> struct PoisSmallPlan<32> { static constexpr int TP = 8, TQ = 4, NT = 256; };
+template <> struct PoisSmallPlan<48> { static constexpr int TP = 8, TQ = 6, NT = 256; };
+template <> struct PoisSmallPlan<64> { static constexpr int TP = 8, TQ = 8, NT = 256; };
+template <> struct PoisSmallPlan<80> { static constexpr int TP = 16, TQ = 5, NT = 256; };
+template <> struct PoisSmallPlan<96> { static constexpr int TP = 16, TQ = 6, NT = 512; };
+template <> struct PoisSmallPlan<112> { static constexpr int TP = 16, TQ = 7, NT = 512; };
 
 // ---------------------------------------------------------------- fused Gaussian init at 160^2
 // init_l2 (models/Unrolled_ADMM.py:170-175), the Gaussian constants and F(x0) in one launch, one 512-thread
@@ -2637,6 +2674,8 @@ __global__ __launch_bounds__(subnet::kThreads, GD_SN_WPE) void k_subnet_rhos_ini
                                                                         int n_out, int map) {
     static_assert(SmallInitLds<L, subnet::kThreads>::SIZE * 8 <= (subnet::kRegionA + subnet::kRegionB) * 4,
                   "the init's LDS inside the SubNet's");
+    static_assert(PoisInitLds<L, PoisSmallPlan<L>::TP, PoisSmallPlan<L>::TQ, subnet::kThreads>::SIZE * 8 <=
+                      (subnet::kRegionA + subnet::kRegionB) * 4, "the Poisson init's LDS inside the SubNet's");
     __shared__ __attribute__((aligned(16))) float AB[subnet::kRegionA + subnet::kRegionB];
     const int b = blockIdx.x;
     int g, init;
@@ -2653,6 +2692,9 @@ __global__ __launch_bounds__(subnet::kThreads, GD_SN_WPE) void k_subnet_rhos_ini
     }
     if (g >= a.N) return;  // uniform per block; no barrier crossed
     if (!init) subnet::rhos_body(psf, psf_gstride, h, params, mlp, alpha, alpha_stride, rhos, n_out, AB, g, threadIdx.x);
+    else if (a.llh == GD_LLH_POISSON)  // the SPLIT Poisson init (state layout 4: reads no rho; LDS inside the SubNet's)
+        pois_small_init_body<L, PoisSmallPlan<L>::TP, PoisSmallPlan<L>::TQ, subnet::kThreads, true>(
+            a, g, threadIdx.x, reinterpret_cast<float2*>(AB));
     else gal_small_init_body<L, subnet::kThreads>(a, g, threadIdx.x, reinterpret_cast<float2*>(AB));
 }
 
@@ -3194,34 +3236,39 @@ int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
     return for_chunks_hw(a, L, L, st, std::forward<F>(f));
 }
 
-// k_pois_small's line plans (TP lanes x TQ points, threads).  Not at 128^2: there both images fill 152 KiB of LDS,
-// one 256-thread workgroup per CU, and the chain's kernels were faster (4096 galaxies: 1.33 vs 0.95 ms per
-// iteration; profiles/r04pois_*); at 64^2 / 96^2 / 112^2 the fused form takes 0.82 / 0.95 / 0.46 of the chain's time
-template <int L>
-struct PoisSmallPlan;
-template <> struct PoisSmallPlan<32> { static constexpr int TP = 8, TQ = 4, NT = 256; };
-template <> struct PoisSmallPlan<48> { static constexpr int TP = 8, TQ = 6, NT = 256; };
-template <> struct PoisSmallPlan<64> { static constexpr int TP = 8, TQ = 8, NT = 256; };
-template <> struct PoisSmallPlan<80> { static constexpr int TP = 16, TQ = 5, NT = 256; };
-template <> struct PoisSmallPlan<96> { static constexpr int TP = 16, TQ = 6, NT = 512; };
-template <> struct PoisSmallPlan<112> { static constexpr int TP = 16, TQ = 7, NT = 512; };
 #ifndef GD_POIS_SMALL
 #define GD_POIS_SMALL 1  // 1: Poisson iterations at L <= 112 in one launch (k_pois_small); 0: the three-kernel chain
 #endif
+// Poisson state layouts (gd_admm_state_layout): 3 = [OTF | u1 | w] with w = v1 - 0 after the init; 4 = the same
+// buffers, the init SPLIT (w slot = H x0 until iteration 0 forms w1): the fused small path (L <= 112 square, fused
+// init and iterations on) - the init then reads no rho and runs beside the SubNet
+inline bool pois_split(int H, int W) {
+    return GD_POIS_SMALL && g_fused && g_fused_init && H == W &&
+           (H == 32 || H == 48 || H == 64 || H == 80 || H == 96 || H == 112);
+}
 template <int L>
 int pois_small_init_launch(const Args& a, hipStream_t st) {
     using PL = PoisSmallPlan<L>;
     ProfScope ps("k_pois_small_init<" + std::to_string(L) + ">", st);
-    hipLaunchKernelGGL((k_pois_small_init<L, PL::TP, PL::TQ, PL::NT>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    if (pois_split(L, L)) hipLaunchKernelGGL((k_pois_small_init<L, PL::TP, PL::TQ, PL::NT, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    else hipLaunchKernelGGL((k_pois_small_init<L, PL::TP, PL::TQ, PL::NT, false>), dim3(a.N), dim3(PL::NT), 0, st, a);
     return check_launch("k_pois_small_init");
 }
 template <int L>
 int pois_small_launch(const Args& a, hipStream_t st) {
     using PL = PoisSmallPlan<L>;
-    static const std::string names[2] = {"k_pois_small<" + std::to_string(L) + ",MID>", "k_pois_small<" + std::to_string(L) + ",LAST>"};
-    ProfScope ps(names[a.last ? 1 : 0], st);
-    if (a.last) hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
-    else hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, false>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    static const std::string names[4] = {"k_pois_small<" + std::to_string(L) + ",MID>", "k_pois_small<" + std::to_string(L) + ",FIRST>",
+                                         "k_pois_small<" + std::to_string(L) + ",LAST>",
+                                         "k_pois_small<" + std::to_string(L) + ",FIRST_LAST>"};
+    const bool first = a.first && pois_split(L, L);  // iteration 0 after a SPLIT init forms w1
+    ProfScope ps(names[first + 2 * a.last], st);
+    if (first) {
+        if (a.last) hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, true, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
+        else hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, false, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    } else {
+        if (a.last) hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, true>), dim3(a.N), dim3(PL::NT), 0, st, a);
+        else hipLaunchKernelGGL((k_pois_small<L, PL::TP, PL::TQ, PL::NT, false>), dim3(a.N), dim3(PL::NT), 0, st, a);
+    }
     return check_launch("k_pois_small");
 }
 
@@ -3643,13 +3690,14 @@ int gd_admm_state_layout(int H, int W, int llh) {
     if (!gd_supported_size(H, W)) return GD_ERR_UNSUPPORTED;
     if (llh == GD_LLH_GAUSSIAN) return 1;
     if (llh != GD_LLH_POISSON) return GD_ERR_ARG;
-    return pois_two_pass(H, W, llh) ? 2 : 3;
+    return pois_two_pass(H, W, llh) ? 2 : (pois_split(H, W) ? 4 : 3);
 }
 
 int gd_admm_init_reads_rho(int H, int W, int llh) {
     if (!gd_supported_size(H, W)) return GD_ERR_UNSUPPORTED;
     if (llh == GD_LLH_GAUSSIAN) return 0;  // iteration 0 forms W~1 (w1_value)
-    return llh == GD_LLH_POISSON ? 1 : GD_ERR_ARG;
+    if (llh != GD_LLH_POISSON) return GD_ERR_ARG;
+    return pois_split(H, W) ? 0 : 1;       // layout 4: iteration 0 forms w1 (k_pois_small<FIRST>)
 }
 
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
@@ -3658,7 +3706,7 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     GD_TRY(check_shape(N, H, W));
     GD_TRY(check_psf(h, w, H, W));
     if (llh != GD_LLH_GAUSSIAN && llh != GD_LLH_POISSON) return fail(GD_ERR_ARG, "llh must be Gaussian or Poisson");
-    if (llh == GD_LLH_POISSON && rho2 == nullptr)
+    if (llh == GD_LLH_POISSON && rho2 == nullptr && !pois_split(H, W))
         return fail(GD_ERR_ARG, "the Poisson init takes the first V step: it needs rho2");
     if (N == 0) return GD_OK;
     Args a = base_args(N, ws, H, W);
@@ -3975,7 +4023,8 @@ int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const flo
 }
 
 int gd_admm_init_subnet_supported(int N, int H, int W, int h, int w, int llh, int n_out) {
-    if (llh != GD_LLH_GAUSSIAN || H != W || !(H == 32 || H == 48 || H == 64) || !g_fused) return 0;
+    if (H != W || !(H == 32 || H == 48 || H == 64) || !g_fused) return 0;
+    if (llh != GD_LLH_GAUSSIAN && !(llh == GD_LLH_POISSON && pois_split(H, W))) return 0;
     if (h != w || h < 2 || (h & 1) || h > gd::subnet::kPsfMaxH || h > H) return 0;
     return N >= 1 && N <= g_subnet_fused_max && n_out >= 1 && n_out <= gd::subnet::kMaxOut;
 }
@@ -3993,7 +4042,7 @@ int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride,
     a.llh = llh;
     bind_state(a, state, N, H, W, llh);
     a.o2 = zin;
-    ProfScope ps("op_admm_init_subnet<" + std::to_string(H) + ",0>", (hipStream_t)stream, 1);
+    ProfScope ps("op_admm_init_subnet<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     const int map = g_sri_map;
     const dim3 grid(map == 1 ? 2 * ((N + 7) / 8 * 8) : 2 * N), block(gd::subnet::kThreads);
 #define GD_SRI_LAUNCH(LL)                                                                                            \

@@ -572,13 +572,14 @@ class ADMMState:
         self.layout = None
         self.iter = 0
         self._side = None   # the side stream an init_concurrent() is running on, until joined
-        key = (self.H, self.W, self.llh)
-        r = ADMMState._reads_rho.get(key)
+        # not cached: for Poisson it follows the fused-path switches (state layout 4: iteration 0 forms w1);
+        # _reads_rho holds overrides only (tests force the serial order with it)
+        r = ADMMState._reads_rho.get((self.H, self.W, self.llh))
         if r is None:
-            r = ADMMState._reads_rho[key] = int(self.lib.gd_admm_init_reads_rho(self.H, self.W, self.llh))
+            r = int(self.lib.gd_admm_init_reads_rho(self.H, self.W, self.llh))
         self.init_reads_rho = r > 0
 
-    _reads_rho = {}     # (H, W, llh) -> gd_admm_init_reads_rho
+    _reads_rho = {}     # (H, W, llh) -> forced gd_admm_init_reads_rho (overrides for tests; empty by default)
     _state_bytes = {}   # (N, H, W, llh) -> gd_admm_state_bytes (pure in its arguments)
     _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (created once)
 

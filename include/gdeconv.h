@@ -94,7 +94,7 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
  *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].  llh = Gaussian: the
  *               first V step is formed by iteration 0 (gd_admm_iter's rho2 is rho2_iters[..., 0]), so
  *               the init reads no rho (rho2 may be NULL) and may run while the SubNet computes the
- *               schedule (gd_admm_init_reads_rho).
+ *               schedule (gd_admm_init_reads_rho); likewise Poisson in state layout 4.
  * gd_admm_iter: one loop body after the denoiser produced z from zin (iter = 0-based index):
  *               X update, duals, then (unless last) the next V step with rho2_next and the next
  *               denoiser input x + u1 -> zin_or_out; last != 0 -> zin_or_out = x (times alpha for
@@ -102,12 +102,14 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
 size_t gd_admm_state_bytes(int N, int H, int W, int llh);
 /* Which state layout gd_admm_init would write NOW for (H, W, llh): 1 = Gaussian spectral, 2 = Poisson
  * in two whole-galaxy passes (256^2 with a fused iteration: [|H|^2 | H | U1 | W~ | X] + w), 3 = Poisson
- * three-kernel ([otf | u1 | w]); negative = unsupported.  The Poisson layout follows
- * gd_set_fused_iteration, so a caller records it at init and checks it before each gd_admm_iter (a
- * toggle in between would bind a different layout than the init wrote). */
+ * three-kernel ([otf | u1 | w]), 4 = Poisson at square L <= 112 with the fused init and iteration (the
+ * buffers of 3; the init leaves H x0 in the w slot and reads no rho, iteration 0 forms w1 with its rho2);
+ * negative = unsupported.  The Poisson layout follows gd_set_fused_iteration / gd_set_fused_init, so a
+ * caller records it at init and checks it before each gd_admm_iter (a toggle in between would bind a
+ * different layout than the init wrote). */
 int gd_admm_state_layout(int H, int W, int llh);
-/* 1 if gd_admm_init reads its rho2 argument for (H, W, llh) (Poisson: the first V step is taken in
- * the init), 0 if it does not (Gaussian, every size), negative = unsupported. */
+/* 1 if gd_admm_init reads its rho2 argument for (H, W, llh) (Poisson layouts 2 and 3: the first V step
+ * is taken in the init), 0 if it does not (Gaussian, every size; Poisson layout 4), negative = unsupported. */
 int gd_admm_init_reads_rho(int H, int W, int llh);
 int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h, int w,
                  const float* alpha, long long alpha_stride, const float* rho2, long long rho2_stride,
@@ -194,9 +196,9 @@ int gd_subnet_rhos_psf(const float* psf, long long psf_gstride, int h, const flo
                        const float* alpha, long long alpha_stride, float* feat, float* rhos, int n_out, int N,
                        void* stream);
 
-/* gd_admm_init (llh = Gaussian) and gd_subnet_rhos_psf of the same batch in ONE launch: the SubNet's
- * workgroups and the init's share the CUs (models/Unrolled_ADMM.py:177-196, the rhos of :77-90 and
- * init_l2 :170-175; the Gaussian init reads no rho, so the two are independent).  For small square
+/* gd_admm_init (llh = Gaussian, or Poisson in state layout 4) and gd_subnet_rhos_psf of the same batch in
+ * ONE launch: the SubNet's workgroups and the init's share the CUs (models/Unrolled_ADMM.py:177-196, the
+ * rhos of :77-90 and init_l2 :170-175; those inits read no rho, so the two are independent).  For small square
  * images (32, 48, 64: the LSST stamps of configs[1]) and batches of at most the fused-SubNet limit;
  * gd_admm_init_subnet_supported says whether a call is fusable, otherwise the call returns
  * GD_ERR_UNSUPPORTED and the caller runs the two entry points.  Results are bit-identical to the pair. */

@@ -365,13 +365,15 @@ def test_configs1_full_batch_48(dev):
     assert report("configs[1] 256 x 48^2 n=8 Gaussian full model, 3-galaxy oracle spot-check", out[idx], ref) < TOL
 
 
-@pytest.mark.parametrize("L,N", [(48, 256), (32, 100), (256, 64), (80, 40)])
-def test_init_overlap_bit_identical(dev, monkeypatch, L, N):
-    """The Gaussian init reads no rho (iteration 0 forms W~1), so the drop-in overlaps it with the SubNet:
-    at 32^2 / 48^2 both run in ONE launch (gd_admm_init_subnet, their workgroups sharing the CUs), at other
-    sizes the init runs on a side stream while the SubNet runs on the current one.  Either way the output
-    is bit-identical to the serial order (SubNet, then init, on the current stream), eager and under a
-    hipGraph replay of the whole forward."""
+@pytest.mark.parametrize("L,N,llh", [(48, 256, "Gaussian"), (32, 100, "Gaussian"), (256, 64, "Gaussian"),
+                                     (80, 40, "Gaussian"), (48, 256, "Poisson"), (32, 100, "Poisson"),
+                                     (80, 40, "Poisson")])
+def test_init_overlap_bit_identical(dev, monkeypatch, L, N, llh):
+    """The Gaussian init reads no rho (iteration 0 forms W~1), nor does the Poisson init at L <= 112 (state layout
+    4: iteration 0 forms w1), so the drop-in overlaps it with the SubNet: at 32^2 / 48^2 both run in ONE launch
+    (gd_admm_init_subnet, their workgroups sharing the CUs), at other sizes the init runs on a side stream while
+    the SubNet runs on the current one.  Either way the output is bit-identical to the serial order (SubNet,
+    then init, on the current stream), eager and under a hipGraph replay of the whole forward."""
     from gdeconv import _lib, engine, models
     from gdeconv.graphs import GraphedForward
     from gdeconv.models import Unrolled_ADMM
@@ -379,13 +381,14 @@ def test_init_overlap_bit_identical(dev, monkeypatch, L, N):
     from gdeconv.weights import make_state_dict
     lib = _lib.load()
     monkeypatch.setattr(models, "CONCURRENT_INIT_PIXELS", 0)     # overlap at every batch size here
-    G = _lib.GD_LLH["Gaussian"]
-    assert lib.gd_admm_init_reads_rho(L, L, G) == 0
-    assert lib.gd_admm_init_reads_rho(L, L, _lib.GD_LLH["Poisson"]) == 1
+    G = _lib.GD_LLH[llh]
+    assert lib.gd_admm_init_reads_rho(L, L, _lib.GD_LLH["Gaussian"]) == 0
+    assert lib.gd_admm_init_reads_rho(L, L, _lib.GD_LLH["Poisson"]) == (0 if L <= 112 else 1)
+    assert lib.gd_admm_state_layout(L, L, _lib.GD_LLH["Poisson"]) == (4 if L <= 112 else 2)
     h = min(48, L)
     assert lib.gd_admm_init_subnet_supported(N, L, L, h, h, G, 8) == (1 if L <= 64 else 0)
     obs, psf, alpha, _ = make_batch(N, L, h=h, seed=515 + L, device=dev)
-    m = Unrolled_ADMM(n_iters=4, llh="Gaussian")
+    m = Unrolled_ADMM(n_iters=4, llh=llh)
     m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
     m = m.to(dev).eval()
     m.Z = torch.nn.Identity()
