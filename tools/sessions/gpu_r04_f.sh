@@ -1,4 +1,4 @@
-# Round-4 final set (engine rev r04.3) (tag $1): gpu_r04_final.sh (all GPU tests, smoke, PMC passes, kernel stats
+# Round-4 final set (engine rev r04.4) (tag $1): gpu_r04_final.sh (all GPU tests, smoke, PMC passes, kernel stats
 # at 256^2 and 48^2, the graphed 48^2 timeline, bench lines 256 / 48 / Poisson / RL), then the 160^2 and gloo
 # 2-rank lines.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; T=${1:-r04f}; mkdir -p $O
