@@ -1974,6 +1974,9 @@ __global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
 // are 16 lanes x 10 points (tline_fft<160, 16, 10>: DFT-10 = 2 x 5, then DFT-16 across the lanes; the inverse
 // back), looped over the 80 row pairs / 81 columns.  The state layout is the generic path's [N][K][L] (what
 // its init writes), the per-bin arithmetic gauss_iter_elem's, so this is a drop-in for the C_G_ITER* chain.
+#ifndef GD_MID_PF
+#define GD_MID_PF 1  // k_gal_mid: the next row pair's z and each column's state loaded ahead of the transforms
+#endif
 #ifndef GD_MID_FUSED
 #define GD_MID_FUSED 1  // 1: Gaussian iterations (and init) at the mid_size sizes in one launch (k_gal_mid); 0: the runtime-planned chains
 #endif
@@ -1995,10 +1998,28 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
     const float* z = a.a0 + (size_t)g * L * L;
     float2 v[G];
 
-    // R: row pair p -> FFT -> packed spectrum PR[kx][p] (lane j < TQ holds kx = j + TQ k1)
-    for (int p = line; p < L / 2; p += LINES) {
+    // R: row pair p -> FFT -> packed spectrum PR[kx][p] (lane j < TQ holds kx = j + TQ k1).  GD_MID_PF: the next
+    // pair's z is loaded while this pair transforms (one galaxy per CU: nothing else hides a round's load latency)
+    // (only where LDS holds one galaxy per CU anyway, NT = 512: at 80^2 the extra registers cost a workgroup per CU)
+    constexpr bool PF = GD_MID_PF && NT == 512;
+    float2 nz[TQ];
+    if (PF && line < L / 2) {
 #pragma unroll
-        for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * p) * L + j + TP * s], z[(2 * p + 1) * L + j + TP * s]);
+        for (int s = 0; s < TQ; ++s) nz[s] = make_float2(z[(2 * line) * L + j + TP * s], z[(2 * line + 1) * L + j + TP * s]);
+    }
+    for (int p = line; p < L / 2; p += LINES) {
+        if constexpr (PF) {
+#pragma unroll
+            for (int s = 0; s < TQ; ++s) v[s] = nz[s];
+            const int pn = p + LINES;
+            if (pn < L / 2) {
+#pragma unroll
+                for (int s = 0; s < TQ; ++s) nz[s] = make_float2(z[(2 * pn) * L + j + TP * s], z[(2 * pn + 1) * L + j + TP * s]);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * p) * L + j + TP * s], z[(2 * p + 1) * L + j + TP * s]);
+        }
         tline_fft<L, TP, TQ, false>(v, j, my, tw);
         if (j < TQ) {
 #pragma unroll
@@ -2012,6 +2033,13 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
     const bool odd = j & 1;
     for (int kx = line; kx < K; kx += LINES) {
         const int km = kx == 0 ? 0 : L - kx;
+        const bool cl = j < TQ;
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+        GState pre[TP];  // (PF) this column's state, in flight during its forward transform
+        if constexpr (PF) {
+#pragma unroll
+            for (int k1 = 0; k1 < TP; ++k1) pre[k1] = gauss_load<L, FIRST, LAST>(a, ob + TQ * k1);
+        }
 #pragma unroll
         for (int s = 0; s < TQ; ++s) {
             const int p = (j >> 1) + (TP / 2) * s;
@@ -2019,11 +2047,11 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
             v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
         }
         tline_fft<L, TP, TQ, false>(v, j, my, tw);
-        const bool cl = j < TQ;
-        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
 #pragma unroll
-        for (int k1 = 0; k1 < TP; ++k1)
-            v[k1] = gauss_iter_elem<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], r1, r2, r2n, cl, inv_n);
+        for (int k1 = 0; k1 < TP; ++k1) {
+            if constexpr (PF) v[k1] = gauss_iter_st<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], pre[k1], r1, r2, r2n, cl, inv_n);
+            else v[k1] = gauss_iter_elem<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], r1, r2, r2n, cl, inv_n);
+        }
         tline_fft<L, TQ, TP, true>(v, j, my, tw);
         const bool self = (kx == 0) || (2 * kx == L);
 #pragma unroll
