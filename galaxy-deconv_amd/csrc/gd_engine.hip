@@ -2103,6 +2103,9 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
 // OTF; writes u1, w, zin: 6 img + 1 half per galaxy against 10 img + 7 half for the chain.
 // FIRST (state layout 4, after a SPLIT init): the w slot holds H x0; the row phase forms w1 = V(H x0 + 0, y, rho2,
 // alpha) there (RI_INIT's arithmetic with this iteration's rho2, the init's rho2_iters[0]) and stores it back
+#ifndef GD_POIS_PF
+#define GD_POIS_PF 1  // k_pois_small: the next row job's inputs loaded ahead of its transform (512-thread plans)
+#endif
 template <int L, int TP, int TQ, int NT, bool LAST, bool FIRST = false>
 __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
     constexpr int G = TP, K = L / 2 + 1, LINES = NT / G, SP = L / 2 + 1, IMS = L * SP;
@@ -2124,21 +2127,41 @@ __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
     __syncthreads();
     float2 v[G], q[G];
 
-    // R: job t < L/2: pair t of z - u1; job t >= L/2: pair t - L/2 of w
+    // R: job t < L/2: pair t of z - u1; job t >= L/2: pair t - L/2 of w.  PF (512 threads, one galaxy per CU): the
+    // next job's inputs are in flight during this job's transform
+    constexpr bool PF = GD_POIS_PF && NT == 512;
+    auto rload = [&](float4 (&b)[TQ], int t) {
+        const int im = t >= L / 2, p = t - im * (L / 2), o0 = (2 * p) * L + j, o1 = o0 + L;
+#pragma unroll
+        for (int s = 0; s < TQ; ++s) {
+            if (im) b[s] = make_float4(wv[o0 + TP * s], wv[o1 + TP * s], FIRST ? a.y[gi + o0 + TP * s] : 0.f,
+                                       FIRST ? a.y[gi + o1 + TP * s] : 0.f);
+            else b[s] = make_float4(z[o0 + TP * s], z[o1 + TP * s], u1[o0 + TP * s], u1[o1 + TP * s]);
+        }
+    };
+    float4 pf[TQ];
+    if (PF && line < L) rload(pf, line);
     for (int t = line; t < L; t += LINES) {
         const int im = t >= L / 2, p = t - im * (L / 2), o0 = (2 * p) * L + j, o1 = o0 + L;
+        float4 cur[TQ];
+        if constexpr (PF) {
+#pragma unroll
+            for (int s = 0; s < TQ; ++s) cur[s] = pf[s];
+            if (t + LINES < L) rload(pf, t + LINES);
+        } else {
+            rload(cur, t);
+        }
 #pragma unroll
         for (int s = 0; s < TQ; ++s) {
             if (FIRST && im) {  // w1 from H x0 (the SPLIT init), stored for the update phase
                 const size_t p0 = gi + o0 + TP * s, p1 = gi + o1 + TP * s;
-                const float w0 = v_step(GD_LLH_POISSON, wv[o0 + TP * s] + 0.0f, fmaxf(a.y[p0], 0.f), r2, al);
-                const float w1 = v_step(GD_LLH_POISSON, wv[o1 + TP * s] + 0.0f, fmaxf(a.y[p1], 0.f), r2, al);
+                const float w0 = v_step(GD_LLH_POISSON, cur[s].x + 0.0f, fmaxf(cur[s].z, 0.f), r2, al);
+                const float w1 = v_step(GD_LLH_POISSON, cur[s].y + 0.0f, fmaxf(cur[s].w, 0.f), r2, al);
                 a.o1[p0] = w0;
                 a.o1[p1] = w1;
                 v[s] = make_float2(w0, w1);
             } else {
-                v[s] = im ? make_float2(wv[o0 + TP * s], wv[o1 + TP * s])
-                          : make_float2(z[o0 + TP * s] - u1[o0 + TP * s], z[o1 + TP * s] - u1[o1 + TP * s]);
+                v[s] = im ? make_float2(cur[s].x, cur[s].y) : make_float2(cur[s].x - cur[s].z, cur[s].y - cur[s].w);
             }
         }
         tline_fft<L, TP, TQ, false>(v, j, my, tw);
@@ -2161,12 +2184,15 @@ __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
             v[s] = odd ? make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x)) : make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
             q[s] = odd ? make_float2(0.5f * (E.y + Fm.y), 0.5f * (Fm.x - E.x)) : make_float2(0.5f * (E.x + Fm.x), 0.5f * (E.y - Fm.y));
         }
+        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
+        float2 hk[TP];  // this column's OTF, in flight during the forward transforms
+#pragma unroll
+        for (int k1 = 0; k1 < TP; ++k1) hk[k1] = a.otf[ob + TQ * k1];
         tline_fft<L, TP, TQ, false>(v, j, my, tw);
         tline_fft<L, TP, TQ, false>(q, j, my, tw);
-        const size_t ob = ((size_t)g * K + kx) * L + (cl ? j : 0);
 #pragma unroll
         for (int k1 = 0; k1 < TP; ++k1) {
-            const float2 Hk = a.otf[ob + TQ * k1];
+            const float2 Hk = hk[k1];
             const float HtH = Hk.x * Hk.x + Hk.y * Hk.y;  // C_ITER's arithmetic
             const float lhs = r1 * HtH + r2;
             const float2 HtW = cmulc(q[k1], Hk);
