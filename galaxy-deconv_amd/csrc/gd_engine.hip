@@ -1999,9 +1999,9 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
     float2 v[G];
 
     // R: row pair p -> FFT -> packed spectrum PR[kx][p] (lane j < TQ holds kx = j + TQ k1).  GD_MID_PF: the next
-    // pair's z is loaded while this pair transforms (one galaxy per CU: nothing else hides a round's load latency)
-    // (only where LDS holds one galaxy per CU anyway, NT = 512: at 80^2 the extra registers cost a workgroup per CU)
-    constexpr bool PF = GD_MID_PF && NT == 512;
+    // pair's z is loaded while this pair transforms (at 144 / 160^2 one galaxy per CU: nothing else hides a round's
+    // load latency; at 80 / 112^2 it costs a workgroup per CU and still wins, r04midnt_ab.txt)
+    constexpr bool PF = GD_MID_PF != 0;
     float2 nz[TQ];
     if (PF && line < L / 2) {
 #pragma unroll
@@ -2104,7 +2104,7 @@ __global__ __launch_bounds__(NT) void k_gal_mid(Args a) {
 // FIRST (state layout 4, after a SPLIT init): the w slot holds H x0; the row phase forms w1 = V(H x0 + 0, y, rho2,
 // alpha) there (RI_INIT's arithmetic with this iteration's rho2, the init's rho2_iters[0]) and stores it back
 #ifndef GD_POIS_PF
-#define GD_POIS_PF 1  // k_pois_small: the next row job's inputs loaded ahead of its transform (512-thread plans)
+#define GD_POIS_PF 1  // k_pois_small: the next row job's inputs loaded ahead of its transform (64^2: 0.188 -> 0.173 ms)
 #endif
 template <int L, int TP, int TQ, int NT, bool LAST, bool FIRST = false>
 __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
@@ -2127,9 +2127,9 @@ __global__ __launch_bounds__(NT) void k_pois_small(Args a) {
     __syncthreads();
     float2 v[G], q[G];
 
-    // R: job t < L/2: pair t of z - u1; job t >= L/2: pair t - L/2 of w.  PF (512 threads, one galaxy per CU): the
-    // next job's inputs are in flight during this job's transform
-    constexpr bool PF = GD_POIS_PF && NT == 512;
+    // R: job t < L/2: pair t of z - u1; job t >= L/2: pair t - L/2 of w.  PF: the next job's inputs are in flight
+    // during this job's transform
+    constexpr bool PF = GD_POIS_PF != 0;
     auto rload = [&](float4 (&b)[TQ], int t) {
         const int im = t >= L / 2, p = t - im * (L / 2), o0 = (2 * p) * L + j, o1 = o0 + L;
 #pragma unroll
@@ -3516,13 +3516,17 @@ struct Ops {
 // lines of 16 lanes (a divisor of the wave) x TQ points (radix 5, 7, 9 = 3 x 3, 10), the packed half spectrum and
 // 32 lines' exchange areas in LDS (144^2: 126 KiB, 160^2: 147 KiB)
 inline bool mid_size(int H, int W) { return H == W && (H == 80 || H == 112 || H == 144 || H == 160); }
-// threads per workgroup: 80^2 (50 KiB of LDS) takes 256, so three galaxies share a CU (VGPRs allow three waves
-// per SIMD); the larger sizes fill the LDS with one galaxy and take 512
-#ifndef GD_MID80_THREADS
-#define GD_MID80_THREADS 256
+// threads per workgroup: 80^2 and 112^2 (38 / 67 KiB of LDS at 256 threads) take 256, so two galaxies share a CU
+// (the prefetching k_gal_mid holds ~210 VGPRs: two waves per SIMD); 144 / 160^2 fill the LDS with one galaxy and
+// take 512 (at 256 threads they ran 0.66 / 0.77 ms per iteration against 0.60 / 0.73, r04midnt_ab.txt)
+#ifndef GD_MID_BIG_THREADS
+#define GD_MID_BIG_THREADS 512  // k_gal_mid / k_gal_mid_init workgroup above 112^2
+#endif
+#ifndef GD_MID_SMALL_THREADS
+#define GD_MID_SMALL_THREADS 256  // ... at 80 and 112^2
 #endif
 template <int L>
-constexpr int mid_threads() { return L <= 80 ? GD_MID80_THREADS : 512; }
+constexpr int mid_threads() { return L <= 112 ? GD_MID_SMALL_THREADS : GD_MID_BIG_THREADS; }
 template <int L>
 int gal_mid_launch_t(const Args& a, hipStream_t st) {
     constexpr int NT = mid_threads<L>(), TP = 16, TQ = L / 16;
