@@ -119,7 +119,7 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         # k_psf_rows<STATE>'s compact row spectra [kx][i] (h (L/2 + 1) complex), written once and read once; the
         # round-3 model counted them twice over (5.70 GB at 4096 x 256^2 against PMC 5.32 GB = 0.93x; now 5.30 GB)
         # (160^2, k_gal_mid_init: the PSF's packed row-pair spectra [L][h/2] parked in the U1 slot, written and read)
-        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L in (80, 112, 144, 160) else 0)
+        rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L in (80, 96, 112, 128, 144, 160) else 0)
         return 2 * img + 2.5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:
@@ -391,9 +391,9 @@ def main():
     fused = lib.gd_set_fused_iteration(0)
     lib.gd_set_fused_iteration(fused)
     generic = args.size not in (32, 48, 64, 96, 128, 256)  # gd_supported_size == 2: gd_generic.hpp
-    # 80 / 112 / 144 / 160 (runtime-planned sizes) run their Gaussian iterations and init fused too (k_gal_mid,
-    # k_gal_mid_init: gd_engine.hip mid_size)
-    mid_fused = bool(fused) and args.size in (80, 112, 144, 160) and args.llh == "Gaussian"
+    # 80 / 112 / 144 / 160 (runtime-planned sizes) and 96 / 128 run their Gaussian iterations and init fused too
+    # (k_gal_mid, k_gal_mid_init: gd_engine.hip mid_size, GD_MID_EXTRA)
+    mid_fused = bool(fused) and args.size in (80, 96, 112, 128, 144, 160) and args.llh == "Gaussian"
     use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian"
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     # Poisson at L <= 112: one workgroup per galaxy, both images in LDS (k_pois_small, k_pois_small_init)
@@ -639,7 +639,7 @@ def main():
                    "ranks_seen": world, "backend": backend or "none",
                    "chunk_mib": chunk_bytes / (1 << 20), "pipeline_streams": pipe_streams if pipelined else 1,
                    "iteration": (("fused, " + (ITER_IMPL[fused] if L == 256 else
-                                               f"k_gal_mid ({L}^2: half spectrum in LDS, 512 threads per galaxy)"
+                                               f"k_gal_mid ({L}^2: half spectrum in LDS, {256 if L <= 112 else 512} threads per galaxy)"
                                                if mid_fused else
                                                "k_gal_small (half spectrum in LDS, one workgroup per galaxy)"))
                                  if use_fused else (rl_impl if rl else
@@ -654,7 +654,7 @@ def main():
                             if (L == 256 and args.llh == "Gaussian") else
                             (("k_psf_rows + k_gal_reg_init<POIS>" if fused_init else "chunked Gaussian chain")
                              + " + k_pois_b<INIT>") if pois2 else
-                            ("fused, k_gal_small_init (one launch)" if L <= 96 and args.llh == "Gaussian" and fused
+                            ("fused, k_gal_small_init (one launch)" if L <= 64 and args.llh == "Gaussian" and fused
                              and not generic else
                              f"fused, k_gal_mid_init ({L}^2: one launch, half spectrum in LDS)" if mid_fused and fused_init
                              else f"fused, k_pois_small_init ({L}^2: one launch, both images in LDS)"

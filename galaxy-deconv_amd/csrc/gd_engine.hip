@@ -3330,6 +3330,14 @@ int pois_small_launch(const Args& a, hipStream_t st) {
 }
 
 // Operation bodies, templated on L.
+#ifndef GD_MID_EXTRA
+#define GD_MID_EXTRA 1  // 1: k_gal_mid / k_gal_mid_init for the compile-time sizes 96 and 128 too (r04midextra_ab.txt: iteration
+                        // 0.346 -> 0.314 / 0.604 -> 0.469 ms, init 0.81 -> 0.43 / 1.00 -> 0.99 ms); k_gal_small stays at 64^2 (0.095 vs 0.168)
+#endif
+template <int L>
+int gal_mid_launch_t(const Args& a, hipStream_t st);
+template <int L>
+int gal_mid_init_launch_t(const Args& a, hipStream_t st);
 template <int L>
 struct Ops {
     static constexpr size_t IMG = (size_t)L * L * 4, HALF = (size_t)(L / 2 + 1) * L * 8;
@@ -3396,6 +3404,9 @@ struct Ops {
     }
     static int admm_init_gauss(Args a0, hipStream_t st0) {
         // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
+        if constexpr (GD_MID_EXTRA && (L == 96 || L == 128)) {
+            if (g_fused && g_fused_init) return gal_mid_init_launch_t<L>(a0, st0);  // k_gal_mid_init
+        }
         if constexpr (L <= 96) {
             if (g_fused) return Lc::gal_small_init(a0, st0);  // both spectra in LDS, one pass
         }
@@ -3425,6 +3436,9 @@ struct Ops {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
         if constexpr (has_fused<L>()) {
             if (g_fused) return Lc::gal_iter(a, st0, g_fused);  // one pass, no workspace
+        }
+        if constexpr (GD_MID_EXTRA && (L == 96 || L == 128)) {
+            if (g_fused) return gal_mid_launch_t<L>(a, st0);  // k_gal_mid
         }
         if constexpr (L <= 128) {
             if (g_fused) return Lc::gal_small(a, st0);  // whole spectrum in LDS, one pass
@@ -3516,14 +3530,14 @@ struct Ops {
 // lines of 16 lanes (a divisor of the wave) x TQ points (radix 5, 7, 9 = 3 x 3, 10), the packed half spectrum and
 // 32 lines' exchange areas in LDS (144^2: 126 KiB, 160^2: 147 KiB)
 inline bool mid_size(int H, int W) { return H == W && (H == 80 || H == 112 || H == 144 || H == 160); }
-// threads per workgroup: 80^2 and 112^2 (38 / 67 KiB of LDS at 256 threads) take 256, so two galaxies share a CU
+// threads per workgroup: 80, 96 and 112^2 (38 / 52 / 67 KiB of LDS at 256 threads) take 256, so two galaxies share a CU
 // (the prefetching k_gal_mid holds ~210 VGPRs: two waves per SIMD); 144 / 160^2 fill the LDS with one galaxy and
-// take 512 (at 256 threads they ran 0.66 / 0.77 ms per iteration against 0.60 / 0.73, r04midnt_ab.txt)
+// take 512 (at 256 threads they ran 0.66 / 0.77 ms per iteration against 0.60 / 0.73, r04midnt_ab.txt), as does 128^2
 #ifndef GD_MID_BIG_THREADS
 #define GD_MID_BIG_THREADS 512  // k_gal_mid / k_gal_mid_init workgroup above 112^2
 #endif
 #ifndef GD_MID_SMALL_THREADS
-#define GD_MID_SMALL_THREADS 256  // ... at 80 and 112^2
+#define GD_MID_SMALL_THREADS 256  // ... at 80, 96 and 112^2
 #endif
 template <int L>
 constexpr int mid_threads() { return L <= 112 ? GD_MID_SMALL_THREADS : GD_MID_BIG_THREADS; }
@@ -3633,7 +3647,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r04.5"; }
+const char* gd_engine_rev(void) { return "r04.6"; }
 
 // the source hash __graft_entry__.build() computed (gdeconv._lib.source_hash); the "gdsrc:" marker lets the
 // build find it in the binary without loading it

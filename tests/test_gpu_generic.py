@@ -372,10 +372,10 @@ def test_fused_poisson_small_matches_chain_and_oracle(dev, L, n):
     assert e_f < TOL
 
 
-@pytest.mark.parametrize("L", [80, 112, 144, 160])
+@pytest.mark.parametrize("L", [64, 80, 96, 112, 128, 144, 160])
 @pytest.mark.parametrize("n", [0, 1, 2, 4])
 def test_generic_fused_mid_matches_chain_and_oracle(dev, L, n):
-    """80^2 / 112^2 / 144^2 / 160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum
+    """64^2 ... 160^2 Gaussian iterations in one launch per iteration (k_gal_mid: the half spectrum
     in LDS, 16-lane x L/16-point line transforms with radix 5, 7, 9, 10) and the init in one launch
     (k_gal_mid_init) against the runtime-planned chains (gd_set_fused_iteration(0), gd_set_fused_init(0)) and the
     fp64-capable oracle: n = 0 is init_l2 alone (x0), then first / middle / last / first-and-last iterations,
