@@ -42,10 +42,11 @@ def pretty(kname):
     m = re.search(r"k_gal_mid_init<(\d+),", kname)
     if m:
         return f"k_gal_mid_init<{m.group(1)}>"        # fused init at the mid sizes (80 / 112 / 144 / 160)
-    m = re.search(r"k_gal_(?:small_t|small_p|mid)<(\d+), \d+, \d+(?:, \d+)?, (true|false), (true|false)>", kname)
-    if m:  # the transposing-plan small-image iteration: same role (and names) as k_gal_small
-        first, last = m.group(2) == "true", m.group(3) == "true"
-        return f"k_gal_small<{m.group(1)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
+    m = re.search(r"k_gal_(small_t|small_p|mid)<(\d+), \d+, \d+(?:, \d+)?, (true|false), (true|false)>", kname)
+    if m:  # the transposing-plan iterations: k_gal_small's role names (48^2), k_gal_mid's own (80..160^2)
+        first, last = m.group(3) == "true", m.group(4) == "true"
+        base = "k_gal_mid" if m.group(1) == "mid" else "k_gal_small"
+        return f"{base}<{m.group(2)},{['MID', 'FIRST', 'LAST', 'FIRST_LAST'][first + 2 * last]}>"
     m = re.search(r"k_gal_small<(\d+), (true|false), (true|false)>", kname)
     if m:
         first, last = m.group(2) == "true", m.group(3) == "true"
@@ -143,7 +144,8 @@ def main():
     members = [f"k_row_fwd<{L},ONE>", f"k_col<{L},G_ITER>", f"k_col<{L},G_ITER_F>", f"k_col<{L},G_ITER_L>",
                f"k_row_inv<{L},OUT1>", f"k_gal_iter<{L},MID>", f"k_gal_iter<{L},FIRST>", f"k_gal_iter<{L},LAST>",
                f"k_gal_reg<{L}>", f"k_gal_small<{L},MID>", f"k_gal_small<{L},FIRST>", f"k_gal_small<{L},LAST>",
-               f"k_gal_small<{L},FIRST_LAST>"]
+               f"k_gal_small<{L},FIRST_LAST>", f"k_gal_mid<{L},MID>", f"k_gal_mid<{L},FIRST>", f"k_gal_mid<{L},LAST>",
+               f"k_gal_mid<{L},FIRST_LAST>"]
     tot = sum(v["hbm_bytes_per_launch"] * v["launches"] for k, v in out["kernels"].items() if k in members)
     if tot:
         out["kernels"][f"op_admm_iter<{L},Gaussian>"] = {
