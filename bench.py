@@ -65,8 +65,6 @@ MODE_NAMES = {
     "k_subnet_features": ["FEATURES", "PSF"],
     "k_subnet_rhos": ["-", "-", "FUSED"],
     "k_subnet_mlp": ["MLP"],
-    "k_gal_iter": ["MID", "FIRST", "LAST", "FIRST_LAST"],
-    "k_gal_iter2": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_reg": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_small": ["MID", "FIRST", "LAST", "FIRST_LAST"],
     "k_gal_init": ["-", "Y", "W1", "ONE", "REG", "POIS"],
@@ -75,10 +73,8 @@ MODE_NAMES = {
     "k_psf_rows": ["ROWS", "STATE"],
 }
 # fused Gaussian iteration / init implementations (gd_set_fused_iteration / gd_set_fused_init)
-ITER_IMPL = {1: "k_gal_reg (512 threads, nothing parked in global memory)", 2: "k_gal_iter2 (register transposes)",
-             3: "k_gal_iter (1024 threads, parks registers in the output image)"}
-INIT_IMPL = {1: "k_psf_rows + k_gal_reg_init (one launch)", 2: "k_psf_rows + k_gal_iter<KM=1> + k_gal_w1",
-             3: "k_psf_rows + k_gal_iter<KM=3> (one launch)"}
+ITER_IMPL = {1: "k_gal_reg (512 threads, nothing parked in global memory)"}
+INIT_IMPL = {1: "k_psf_rows + k_gal_reg_init (one launch)"}
 
 
 def pretty(name):
@@ -155,9 +151,9 @@ def kernel_bytes(name, L, n_iters):
         f"k_col<{L},G_ITER_F>": half * 6.5,                                 # T, |H|^2, G, W~ -> U1, W~, T
         f"k_col<{L},G_ITER_L>": half * 4.5,                                 # T, |H|^2, U1, W~ -> T
         f"k_col<{L},G_W1>": half * 3.5,                                     # x0 T, |H|^2, G -> W~
-        f"k_gal_iter<{L},MID>": 2 * img + 5.5 * half,                       # z, |H|^2, G, U1, W~ -> U1, W~, zin
-        f"k_gal_iter<{L},FIRST>": 2 * img + 4.5 * half,
-        f"k_gal_iter<{L},LAST>": 2 * img + 2.5 * half,
+        f"k_gal_reg<{L},MID>": 2 * img + 5.5 * half,                        # z, |H|^2, G, U1, W~ -> U1, W~, zin
+        f"k_gal_reg<{L},FIRST>": 2 * img + 4.5 * half,
+        f"k_gal_reg<{L},LAST>": 2 * img + 2.5 * half,
         f"k_row_inv<{L},OUT1>": half + img,                                 # T -> zin | x
         f"k_row_fwd<{L},YA>": img + half,                                   # y -> T
         f"k_col<{L},G_INIT>": half + 2.5 * half,                            # T -> |H|^2, G, T (PSF: 9 KB)
@@ -249,11 +245,13 @@ def parse():
                    help="Infinity-Cache chunk working set in MiB (0 = off; default: library default)")
     p.add_argument("--pipe-streams", type=int, default=None, help="internal HIP streams for chunk pipelining")
     p.add_argument("--fused-init", type=int, default=None,
-                   help="Gaussian init at 256^2: 1 k_gal_reg_init (one launch), 2 k_gal_iter<KM=1> + k_gal_w1, "
-                        "3 k_gal_iter<KM=3>, 0 chunked five-kernel chain")
+                   help="Gaussian init: 1 the one-launch kernels (256^2: k_psf_rows + k_gal_reg_init), 0 the chunked chain")
     p.add_argument("--fused", type=int, default=None,
-                   help="Gaussian iteration: 1 k_gal_reg (256^2; k_gal_small at <= 128), 2 k_gal_iter2, "
-                        "3 k_gal_iter (parking), 0 three kernels")
+                   help="iterations: 1 the one-launch kernels (256^2: k_gal_reg), 0 the chained path")
+    p.add_argument("--settle-s", type=float, default=2.0,
+                   help="after the warmup steps, untimed steps until this many seconds of load (clock settling)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="default run only: skip the configs[1] / configs[4] sub-lines")
     p.add_argument("--traffic-json", default=None,
                    help="rocprofv3 --pmc summary (per-kernel HBM bytes) for the roofline 'traffic' field "
                         "(default: profiles/pmc_traffic.json, _48 / _rl variants for those workloads)")
@@ -362,7 +360,6 @@ def main():
         sys.exit(spawn_ranks(args, sys.argv[1:]))
     from gdeconv import _lib
     from gdeconv.dist import init_process_group, local_device
-    from gdeconv.synth import make_batch
 
     rank, world, local = init_process_group()
     if world != args.gpus:
@@ -378,6 +375,32 @@ def main():
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     lib = _lib.load()
+    ctx = {"lib": lib, "rank": rank, "world": world, "backend": backend, "dev": dev}
+    rec = measure(args, ctx)
+    # the other BASELINE configs a single GPU runs, as sub-lines of the default run (each with its own
+    # step count, roofline and CPU baseline): configs[1] (256 x 48^2) and configs[4] (RL(100), 4096 x 256^2)
+    if world == 1 and not args.no_extra and args.workload == "admm" and args.size == 256 and args.llh == "Gaussian":
+        for key, over in (("configs1", dict(batch=256, size=48, n_iters=8, steps=max(200, args.steps),
+                                            warmup=max(20, args.warmup), settle_s=0.5, no_ingest=True,
+                                            no_e2e=True, cpu_sample=64)),
+                          ("configs4", dict(workload="rl", batch=4096, size=256, n_iters=100, steps=args.steps,
+                                            warmup=min(2, args.warmup), settle_s=1.0, no_ingest=True, no_e2e=True,
+                                            no_graph=True, cpu_sample=4))):
+            sub = argparse.Namespace(**{**vars(args), **over, "traffic_json": None})
+            torch.cuda.empty_cache()
+            rec[key] = measure(sub, ctx)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def measure(args, ctx):
+    """One workload (args.workload / size / batch / n_iters / llh) on this rank: warm-up, clock settling, the
+    timed K steps, the profiling pass, and the fields beside value.  Returns the record (rank 0's is printed)."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib, rank, world, backend, dev = ctx["lib"], ctx["rank"], ctx["world"], ctx["backend"], ctx["dev"]
     if args.chunk_mb is not None:
         lib.gd_set_chunk_bytes(int(args.chunk_mb * (1 << 20)))
     chunk_bytes = lib.gd_set_chunk_bytes(0)
@@ -429,6 +452,17 @@ def main():
         for _ in range(args.warmup):
             out = step()
         torch.cuda.synchronize()
+        # clock settling: the chip's clocks and HBM rate drift for the first ~second of sustained load (round 4:
+        # value 312.8 k against 296 k in the same run's later interleaved blocks), so more untimed steps run
+        # until --settle-s seconds of this workload have passed; reported as clock_settle, apart from warmup
+        ts, settle = time.perf_counter(), 0
+        while time.perf_counter() - ts < args.settle_s:
+            out = step()
+            settle += 1
+            if settle % 4 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        settle_s = time.perf_counter() - ts
         if world > 1:
             dist.barrier()
         # the timed region: no profiling events (value is the clean rate)
@@ -628,7 +662,10 @@ def main():
     rec = {
         "metric": metric,
         "value": gal_s, "unit": "galaxies/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "warmup": args.warmup, "clock_settle": {"steps": settle, "seconds": settle_s,
+                                                "note": "untimed steps after the warmup steps, until --settle-s "
+                                                        "seconds of sustained load had passed"},
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (gdeconv.synth, seeded); deterministic random weights (gdeconv.weights)",
         "config": {"workload": workload,
@@ -685,6 +722,8 @@ def main():
         rec["with_gather"] = with_gather
     if graphed is not None:
         rec["graphed"] = graphed
+        # value (the first timed block) against the same run's later interleaved eager blocks
+        rec["value_vs_interleaved_eager"] = gal_s / graphed["eager_interleaved"]["value"] - 1.0
     if ingest is not None:
         rec["ingest"] = ingest
 
@@ -717,10 +756,7 @@ def main():
         rec["cpu_baseline"] = cpu_baseline(args)
         if world > 1:
             rec["cpu_baseline"]["note"] = "rank 0, after every rank's timed and collective work"
-    if rank == 0:
-        print(json.dumps(rec), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return rec
 
 
 if __name__ == "__main__":

@@ -27,10 +27,10 @@
 //                                                          C_CONVC, RIF_RL_UPDATE / RI_RL_FINAL, C_CONV
 //
 // Whole-galaxy kernels (one workgroup per galaxy, spectra on chip) for the Gaussian ADMM path:
-//   k_gal_iter / k_gal_iter2 (256^2, registers + LDS, slices of 64 columns), k_gal_iter<KM = 1> +
-//   k_gal_w1 (init at 256^2), k_gal_small (iteration, L <= 128, half spectrum in LDS),
-//   k_gal_small_init (init, L <= 96).  The Gaussian state is spectral
-//   (|H|^2, G, U1, W~); the Poisson state below stays spatial.
+//   k_gal_reg / k_gal_reg_init (256^2, registers + LDS, slices of 64 columns; gd_galreg.hpp), k_gal_small
+//   (iteration, 32^2 / 64^2) and k_gal_small_p (48^2), k_gal_small_init (init, L <= 64), k_gal_mid /
+//   k_gal_mid_init (80^2 ... 160^2, multiples of 16).  The Gaussian state is spectral (|H|^2, G, U1, W~;
+//   DESIGN.md section 2); the Poisson state below stays spatial except in the 256^2 two-pass form.
 //
 // Poisson ADMM state carried between iterations (all [N,1,L,L] fp32): u1, w = v - u2, zin (denoiser
 // input) plus y and the half-spectrum OTF.  u2 and v are never stored: u2_{n+1} = Hx_{n+1} - w_n and
@@ -399,7 +399,7 @@ struct ColTraits {
 //   W~'  = V~ - U2~ ;  returns (X + U1') / L^2 (next denoiser input) | X / L^2 (last iteration)
 // First iteration: U1 = 0 (not read); W~ = conj(H) V1 was written by the init (C_G_W1).
 #ifndef GD_RCP_DIV
-#define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % k_gal_iter time)
+#define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % iteration time)
 #endif
 // Streaming (single-use per iteration) state traffic marked non-temporal.  Measured on op_admm_iter:
 // stores (U1, W~, zin) 1.673/1.692 -> 1.658/1.666 ms - on; loads (z, |H|^2, G, U1, W~) 1.75-1.87 ms,
@@ -779,34 +779,6 @@ __global__ __launch_bounds__(256) void k_col(Args a) {
     }
 }
 
-// ---------------------------------------------------------------- fused whole-galaxy Gaussian iteration
-// One 1024-thread workgroup per galaxy, one workgroup per CU: the galaxy's half spectrum (264 KiB at
-// 256^2) lives in that CU's registers and LDS for the whole iteration, so no spectrum goes to HBM:
-// z -> zin moves z, zin and the state (|H|^2, G, U1, W~ read; U1, W~ written), 7.5 fp32 words per
-// pixel instead of the three-kernel path's 11.6.  Phases (S = the LDS union):
-//   R  line l transforms row pairs l and l + 64 (rows 2p + i 2p+1) in registers
-//   A  the bins that columns 0..63 need (X_p[kx], X_p[L - kx]) -> S; line kx gathers its column (the
-//      two rows' half spectra split out of the packed pair); then columns 64..127's bins -> S while
-//      column A is transformed (register-only FFT: S is occupied), updated and transformed back.
-//      Columns 0 and L/2 are real over the rows and ride together in line 0 (see below).
-//   B  gather columns 64..127 from S; column A's results -> S in row layout; column B as column A
-//   I  per half of the rows: column B's results -> S beside column A's (whose other half waits in
-//      registers), row IFFT of the packed pairs, store (x on the last iteration, else zin = x + u1)
-#ifndef GD_FUSED_FFTBAR
-#define GD_FUSED_FFTBAR 1
-#endif
-#ifndef GD_FUSED_NPB
-#define GD_FUSED_NPB 8  // slice-B bin registers (of 8) parked in global memory during column A (fewer: spills)
-#endif
-#ifndef GD_FUSED_GROUP
-#define GD_FUSED_GROUP 4
-#endif
-#ifndef GD_FUSED_LPARK
-#define GD_FUSED_LPARK 2  // parked values per thread kept in the LDS left over (16 KiB) instead of global
-#endif
-#ifndef GD_ITER2_PARKA
-#define GD_ITER2_PARKA 1  // k_gal_iter2: park column A's second half in global memory during column B
-#endif
 // A copy of v the compiler cannot see through: addresses recomputed from it are not CSE'd with
 // (and kept live from) an earlier phase's identical computation (register budget: 128 VGPRs at
 // 1024 threads).
@@ -856,44 +828,6 @@ __device__ __forceinline__ void fused_gather(const float2* S, int c, int j, floa
     }
 }
 
-// Spectral update of column kx (rows ky = j + F1 s of this lane).  The first NPRE bins' state may
-// have been loaded ahead (fused_prefetch, issued before the column's gather and forward FFT so their
-// latency hides under that work); the rest is loaded here in groups of GD_FUSED_GROUP.
-#ifndef GD_FUSED_PRE
-#define GD_FUSED_PRE 0
-#endif
-template <int L, bool FIRST, bool LAST, int NPRE = GD_FUSED_PRE>
-__device__ __forceinline__ void fused_prefetch(const Args& a, GState (&pre)[NPRE > 0 ? NPRE : 1], int g, int kx,
-                                               int j) {
-    using FG = FusedGeo<L>;
-    const size_t ob = ((size_t)g * FG::K + opaque(kx)) * L + opaque(j);
-#pragma unroll
-    for (int s = 0; s < NPRE; ++s) pre[s] = gauss_load<L, FIRST, LAST>(a, ob + FG::F1 * s);
-    __builtin_amdgcn_sched_barrier(0);  // issue them here
-}
-template <int L, bool FIRST, bool LAST, int NPRE = GD_FUSED_PRE>
-__device__ __forceinline__ void fused_update(const Args& a, float2 (&C)[FusedGeo<L>::F2], int g, int kx, int j,
-                                             float r1, float r2, float r2n, const GState (&pre)[NPRE > 0 ? NPRE : 1]) {
-    using FG = FusedGeo<L>;
-    constexpr float inv_n = float(1.0 / double(L * L));
-    j = opaque(j);
-    kx = opaque(kx);
-#if GD_FUSED_FFTBAR
-    __builtin_amdgcn_sched_barrier(0);  // keep the state loads below the FFT (register pressure)
-#endif
-    const size_t ob = ((size_t)g * FG::K + kx) * L;
-#pragma unroll
-    for (int s = 0; s < FG::F2; ++s) {
-        if (s < NPRE)
-            C[s] = gauss_iter_st<L, FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], pre[s < NPRE ? s : 0], r1, r2, r2n, true,
-                                              inv_n);
-        else
-            C[s] = gauss_iter_elem<L, FIRST, LAST>(a, ob + j + FG::F1 * s, C[s], r1, r2, r2n, true, inv_n);
-        if (s >= NPRE && (s - NPRE) % GD_FUSED_GROUP == GD_FUSED_GROUP - 1)
-            __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight
-    }
-}
-
 // Workgroup barrier that orders LDS only: outstanding global loads and stores stay in flight
 // (__syncthreads would drain them at every phase boundary).
 __device__ __forceinline__ void lds_barrier() {
@@ -902,10 +836,9 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// ---- the fused Gaussian init on the same skeleton (KM: 0 = iteration, 1 = init; iteration 0's W~ is
-// k_gal_w1 below)
-//   KM = 1  y -> max(y,0)/alpha -> R, A, B with the OTF column built in-kernel: |H|^2, G (state), X0 =
-//           G / (|H|^2 + 1/alpha) -> inverse -> I: x0 = clamp(., 0, 1) -> zin   (RF_YA, C_G_INIT, RIF_CLAMP)
+// ---- helpers of the fused Gaussian init at 256^2 (k_gal_reg_init, gd_galreg.hpp):
+//   y -> max(y,0)/alpha -> R, A, B with the OTF column built in-kernel: |H|^2, G (state), X0 =
+//   G / (|H|^2 + 1/alpha) -> inverse -> I: x0 = clamp(., 0, 1) -> zin   (RF_YA, C_G_INIT, RIF_CLAMP)
 // The OTF column kx comes from the PSF's compact row spectra (k_psf_rows<L, true>, parked in the U1
 // slot): placed row ky holds psf row i = (ky + h/2) mod L when i < h.  Line 0 carries columns 0 and
 // L/2 (real over the rows) packed as P0 + i P_{L/2}, like the data, and splits them after the FFT.
@@ -954,42 +887,6 @@ __device__ __forceinline__ void init_hcol(float2 (&Hc)[FusedGeo<L>::F2], const f
     Hc[FG::F2 - 2] = h4[2];
     Hc[FG::F2 - 1] = h4[3];
 }
-// The OTF column's FFT runs with register (DPP) transposes while the data column waits in the line's
-// LDS exchange area (register budget: the two columns are never both in registers).  Line 0 splits
-// the packed columns through nyqh (all reads before any write).
-template <int L>
-__device__ __forceinline__ void init_hfft(float2 (&Hc)[FusedGeo<L>::F2], int j, bool l0, const float2* tw,
-                                          float2* nyqh) {
-    using FG = FusedGeo<L>;
-    line_fft<L, false, true, true>(Hc, opaque(j), nullptr, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < FG::F2; ++s) nyqh[j + FG::F1 * s] = Hc[s];
-        wave_lds_sync();
-        float2 zm[FG::F2];
-#pragma unroll
-        for (int s = 0; s < FG::F2; ++s) zm[s] = nyqh[(L - j - FG::F1 * s) & (L - 1)];
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < FG::F2; ++s) {
-            const float2 z = Hc[s];
-            nyqh[j + FG::F1 * s] = make_float2(0.5f * (z.y + zm[s].y), 0.5f * (zm[s].x - z.x));
-            Hc[s] = make_float2(0.5f * (z.x + zm[s].x), 0.5f * (z.y - zm[s].y));
-        }
-    }
-}
-template <int L>
-__device__ __forceinline__ void stash(float2* my, const float2 (&C)[FusedGeo<L>::F2], int j) {
-#pragma unroll
-    for (int s = 0; s < FusedGeo<L>::F2; ++s) my[j + FusedGeo<L>::F1 * s] = C[s];
-    wave_lds_sync();
-}
-template <int L>
-__device__ __forceinline__ void unstash(const float2* my, float2 (&C)[FusedGeo<L>::F2], int j) {
-    wave_lds_sync();
-#pragma unroll
-    for (int s = 0; s < FusedGeo<L>::F2; ++s) C[s] = my[j + FusedGeo<L>::F1 * s];
-}
 // init_l2 (models/Unrolled_ADMM.py:170-175) per bin: |H|^2, G = conj(H) F(max(y,0)/alpha) kept as
 // state; returns X0 / L^2 = G / (|H|^2 + 1/alpha) / L^2 (the arithmetic of k_col<C_G_INIT>)
 template <int L>
@@ -1008,593 +905,6 @@ __device__ __forceinline__ void w1_bin(const Args& a, size_t o, float2 Xk) {
     // F(x0): the first iteration forms W~1 (Poisson two-pass: H F(x0), pass B<INIT>'s input)
     a.s_w[sflat_c<L>(o)] = a.llh == GD_LLH_POISSON ? cmul(a.s_g[sflat_c<L>(o)], Xk) : Xk;
 }
-template <int L, int KM>
-__device__ __forceinline__ void init_update(const Args& a, float2 (&C)[FusedGeo<L>::F2],
-                                            const float2 (&Hc)[KM == 1 ? FusedGeo<L>::F2 : 1], int g, int kx, int j,
-                                            float al) {
-    using FG = FusedGeo<L>;
-    constexpr float inv_n = float(1.0 / double(L * L));
-    j = opaque(j);
-    kx = opaque(kx);
-    __builtin_amdgcn_sched_barrier(0);
-    const size_t ob = ((size_t)g * FG::K + kx) * L + j;
-#pragma unroll
-    for (int s = 0; s < FG::F2; ++s) {
-        if constexpr (KM == 1)
-            C[s] = init_bin<L>(a, ob + FG::F1 * s, C[s], Hc[s], al, inv_n);
-        else
-            w1_bin<L>(a, ob + FG::F1 * s, C[s]);
-        if (s % GD_FUSED_GROUP == GD_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// W~'s columns (k_gal_w1) from x0's row spectra in registers (X[q] = pairs line + LINES q): slice A
-// -> S, column A gathered, slice B -> S, column A by register transposes, column B.  S, nyq, nyqc
-// are the caller's LDS (the fused-iteration layout); the caller's exchange areas must be free.
-template <int L>
-__device__ __forceinline__ void w1_columns(const Args& a, float2 (&X)[FusedGeo<L>::PPL][FusedGeo<L>::F2], float2* S,
-                                           float2* nyq, float2* nyqc, const float2* tw, int g, int tid) {
-    using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
-    const int line = tid / F1, j = tid - line * F1;
-    const bool l0 = (line == 0);
-    float2* my = S + line * FG::XCH;
-    lds_barrier();  // exchange areas -> slice A
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        const int p = line + LINES * q;
-        float2* row = S + p * SLD;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            const int k = j + F1 * r;
-            if (r < KS / F1) row[k] = X[q][r];
-            if (r == 0 && j == 0) row[KS] = X[q][r];
-            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];
-            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];
-        }
-    }
-    lds_barrier();
-    float2 C[F2];
-    {  // fused_gather with few LDS loads in flight (slice B is still in registers)
-        const int c = opaque(line), jj = opaque(j);
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int y = jj + F1 * s;
-            const float2 u = S[(y >> 1) * SLD + c], v = S[(y >> 1) * SLD + KS + c];
-            C[s] = (y & 1) ? make_float2(0.5f * (u.y + v.y), 0.5f * (v.x - u.x))
-                           : make_float2(0.5f * (u.x + v.x), 0.5f * (u.y - v.y));
-            const float2 w = nyq[y >> 1];
-            if (l0) C[s].y = (y & 1) ? w.y : w.x;
-            if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    lds_barrier();  // S -> slice B (k_gal_iter's phase-B layout)
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        float2* row = S + (line + LINES * q) * SLD;
-#pragma unroll
-        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
-            const int k = j + F1 * r;
-            if (r < 2 * KS / F1) row[k - KS] = X[q][r];
-            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
-                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];
-            }
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // slice B leaves the registers before the transform
-    line_fft<L, false, true, true>(C, opaque(j), nullptr, tw);
-    if (l0) {  // columns 0 and L/2 out of the packed column (k_gal_iter's split, scratch nyqc)
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqc[j + F1 * s] = C[s];
-        wave_lds_sync();
-        float2 zm[F2];
-#pragma unroll
-        for (int s = 0; s < F2; ++s) zm[s] = nyqc[(L - j - F1 * s) & (L - 1)];
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const float2 z = C[s];
-            nyqc[j + F1 * s] = make_float2(0.5f * (z.y + zm[s].y), 0.5f * (zm[s].x - z.x));
-            C[s] = make_float2(0.5f * (z.x + zm[s].x), 0.5f * (z.y - zm[s].y));
-        }
-    }
-    lds_barrier();  // nyqc and slice B complete
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        w1_bin<L>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid]);
-    const float2 dummy[1] = {make_float2(0.f, 0.f)};
-    init_update<L, 2>(a, C, dummy, g, line, j, 1.f);
-    fused_gather<L>(S, line, j, C);
-    lds_barrier();  // S -> exchange areas
-    line_fft<L, false, true>(C, opaque(j), my, tw);
-    init_update<L, 2>(a, C, dummy, g, KS + line, j, 1.f);
-}
-
-template <int L, bool FIRST, bool LAST, int KM = 0>
-__global__ __launch_bounds__(1024) void k_gal_iter(Args a) {
-    using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, ALD = FG::ALD, LINES = FG::LINES;
-    constexpr float inv_n = float(1.0 / double(L * L));
-    __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
-    __shared__ float nyqo[L];       // x(., L/2)
-    __shared__ float2 nyqh[(KM & 1) ? L : 1];  // init: the OTF's Nyquist column
-    static_assert(KM == 0 || ((KM == 1 || KM == 3) && !FIRST && !LAST), "init variants");
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
-    const bool l0 = (line == 0);
-    float2* my = S + line * FG::XCH;
-    fill_twiddles<L>(tw, tid, FG::THREADS);
-    const float r1 = KM == 0 ? a.rho1(g) : 0.f, r2 = KM == 0 ? a.rho2(g) : 0.f;
-    const float r2n = (LAST || KM != 0) ? 0.f : a.rho2n(g);
-    const float al = (KM & 1) ? a.alpha(g) : 1.f;
-    GD_TRACE(0);
-
-    // R: pair p = line + LINES q  (KM = 1: max(y,0)/alpha, RF_YA)
-    float2 X[FG::PPL][F2];
-    {
-        const float* z = (KM == 0 ? a.a0 : a.y) + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) {
-                if constexpr ((KM & 1))
-                    X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) / al, fmaxf(r0[L + F1 * r], 0.f) / al);
-                else
-                    X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
-            }
-        }
-    }
-    __syncthreads();  // twiddles; all of z loaded (zin may alias z: the park stores below write it)
-    GD_TRACE(1);
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
-    // Register budget (128 VGPRs at 1024 threads; a column's FFTs and update take ~92): what a later
-    // phase needs beyond that is parked in this galaxy's output image, written whole at the end:
-    // region 0 = part of slice B's bins (registers r in [RB0, RB0 + NPB)), region 1 = column A's
-    // results.  Lane-contiguous (512 B per wave instruction),
-    // read back by the same thread; every parked value is read back (and consumed into LDS) before
-    // phase I writes that part of the image.
-    // (KM = 1 parks in zin, its output)
-    float2* park0 = reinterpret_cast<float2*>(((KM & 1) ? a.o2 : a.o0) + (size_t)g * L * L);
-    float2* park1 = park0 + (size_t)L * L / 4;
-    // The LDS the union leaves free holds LP values per thread: slice B's register RB0 (both pairs)
-    // during column A, then column A's results s < LP during column B (the former are restored first).
-    constexpr int LP = GD_FUSED_LPARK;
-    static_assert(LP == 0 || LP == FG::PPL, "one LDS-parked register per pair");
-    __shared__ float2 parkL[LP ? LP : 1][FG::THREADS];
-    constexpr int RB0 = KS / F1, RB1 = (L - KS) / F1;  // r in [RB0, RB1]: slice B bins
-    constexpr int NPB = GD_FUSED_NPB;                   // of which parked
-    static_assert(NPB <= RB1 - RB0 && FG::PPL * NPB * FG::THREADS <= L * L / 4 && F2 * FG::THREADS <= L * L / 4,
-                  "park regions");
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q)
-#pragma unroll
-        for (int r = RB0; r < RB0 + NPB; ++r) {
-            if (LP && r == RB0)
-                parkL[q][tid] = X[q][r];
-            else
-                park0[(q * NPB + r - RB0) * FG::THREADS + tid] = X[q][r];
-        }
-    lds_barrier();  // exchange areas -> slice A
-    GD_TRACE(2);
-
-    // A: bins of columns 0..KS-1 and the Nyquist bins
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        const int p = line + LINES * q;
-        float2* row = S + p * SLD;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            const int k = j + F1 * r;
-            if (r < KS / F1) row[k] = X[q][r];                               // X_p[kx], kx = k
-            if (r == 0 && j == 0) row[KS] = X[q][r];                          // X_p[L - 0]
-            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];                  // X_p[L/2]
-            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];  // X_p[L - kx]
-        }
-    }
-    lds_barrier();
-    GD_TRACE(3);
-    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);  // column A's first bins: in flight under gather + FFT
-    // Columns 0 and L/2 are real sequences over the rows (Re / Im of the pairs' X_p[0], X_p[L/2]):
-    // line 0 carries both as one complex column Z = c_0 + i c_{L/2}, splits the spectra after the
-    // forward FFT (C_0 = (Z + conj Z(-ky))/2, C_{L/2} = (Z - conj Z(-ky))/2i), updates column 0 itself
-    // and hands column L/2 to the first L/64 waves, one element per thread; the results are packed
-    // back the same way, so the inverse FFT's real / imaginary parts are x(., 0) and x(., L/2) (only
-    // real parts are kept for the self-conjugate row bins, as irfft does).
-    float2 Hc[(KM & 1) ? F2 : 1];
-    float2 C[F2];
-    fused_gather<L>(S, line, j, C);
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const int y = j + F1 * s;
-        const float2 w = nyq[y >> 1];
-        if (l0) C[s].y = (y & 1) ? w.y : w.x;
-    }
-    lds_barrier();  // S -> exchange areas
-    GD_TRACE(4);
-    line_fft<L, false, true>(C, opaque(j), my, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) my[j + F1 * s] = C[s];
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int ky = j + F1 * s;
-            const float2 z = C[s], zm = my[(L - ky) & (L - 1)];
-            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
-            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-        }
-        wave_lds_sync();  // (the inverse FFT rewrites the exchange area)
-    }
-    if constexpr ((KM & 1)) {
-        stash<L>(my, C, j);
-        init_hload<L>(a, Hc, g, line, j);
-        init_hfft<L>(Hc, j, l0, tw, nyqh);
-    }
-    lds_barrier();  // nyqc (nyqh) complete
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
-        const size_t on = ((size_t)g * FG::K + L / 2) * L + tid;
-        if constexpr (KM == 0)
-            nyqc[tid] = gauss_iter_elem<L, FIRST, LAST>(a, on, nyqc[tid], r1, r2, r2n, true, inv_n);
-        else
-            nyqc[tid] = init_bin<L>(a, on, nyqc[tid], nyqh[tid], al, inv_n);
-    }
-    if constexpr (KM == 0) {
-        fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
-    } else {
-        unstash<L>(my, C, j);
-        init_update<L, 1>(a, C, Hc, g, line, j, al);
-    }
-    lds_barrier();  // Nyquist results
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const float2 cn = nyqc[j + F1 * s];
-        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
-    }
-    line_fft<L, true, true>(C, opaque(j), my, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
-    }
-    if constexpr (LP > 0) {
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) X[q][RB0] = parkL[q][opaque(tid)];
-    }
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        if (s < LP)
-            parkL[s][tid] = C[s];
-        else
-            park1[s * FG::THREADS + tid] = C[s];
-    }
-    lds_barrier();  // exchange areas -> slice B
-    GD_TRACE(5);
-
-    // B: columns KS..2KS-1
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q)
-#pragma unroll
-        for (int r = RB0 + (LP ? 1 : 0); r < RB0 + NPB; ++r)
-            X[q][r] = park0[(q * NPB + r - RB0) * FG::THREADS + opaque(tid)];
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        float2* row = S + (line + LINES * q) * SLD;
-#pragma unroll
-        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
-            const int k = j + F1 * r;
-            if (r < 2 * KS / F1) row[k - KS] = X[q][r];                       // X_p[kx], kx = k
-            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
-                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];        // X_p[L - kx] at KS + (kx - KS)
-            }
-        }
-    }
-    lds_barrier();
-    GD_TRACE(6);
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
-    float2 Cb[F2];
-    fused_gather<L>(S, line, j, Cb);
-    lds_barrier();
-    GD_TRACE(7);
-    line_fft<L, false, true>(Cb, opaque(j), my, tw);
-    if constexpr (KM == 0) {
-        fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
-    } else {
-        stash<L>(my, Cb, j);
-        init_hload<L>(a, Hc, g, KS + line, j);
-        init_hfft<L>(Hc, j, false, tw, nyqh);
-        unstash<L>(my, Cb, j);
-        init_update<L, 1>(a, Cb, Hc, g, KS + line, j, al);
-    }
-    line_fft<L, true, true>(Cb, opaque(j), my, tw);
-
-    // I: half hf = rows [hf L/2, (hf+1) L/2): both columns' results -> S as row half spectra
-    // [yl][SLD] (bins 0..L/2), row IFFT of the packed pairs, store
-    float* out = ((KM & 1) ? a.o2 : a.o0) + (size_t)g * L * L;
-    float2 Xw[KM == 3 ? FG::PPL : 1][F2];  // KM = 3: row spectra of the clamped x0 (W~'s input)
-    static_for<0, 2>([&](auto hfc) {
-        constexpr int hf = decltype(hfc)::value;
-        lds_barrier();  // exchange areas -> row half spectra
-#pragma unroll
-        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) {
-            float2* rr = S + (j + F1 * s - hf * L / 2) * SLD;
-            const float2 c = s < LP ? parkL[s < LP ? s : 0][opaque(tid)] : park1[s * FG::THREADS + opaque(tid)];
-            rr[line] = make_float2(c.x, l0 ? 0.f : c.y);  // column 0: real part (irfft)
-            rr[KS + line] = Cb[s];
-        }
-        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        lds_barrier();
-        float2 V[F2];
-        {
-            const int jj = opaque(j);
-            const float2* re = S + (2 * opaque(line)) * SLD;
-            const float2* ro = re + SLD;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) {
-                const int k = jj + F1 * r;
-                float2 be, bo;
-                if (k <= L / 2) {
-                    be = re[k];
-                    bo = ro[k];
-                } else {
-                    be = cconj(re[L - k]);
-                    bo = cconj(ro[L - k]);
-                }
-                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
-            }
-        }
-        lds_barrier();  // row half spectra -> exchange areas
-        line_fft<L, true, true>(V, j, my, tw);
-        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            if constexpr ((KM & 1)) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
-                const float2 c = make_float2(fminf(fmaxf(V[r].x, 0.f), 1.f), fminf(fmaxf(V[r].y, 0.f), 1.f));
-                o[F1 * r] = c.x;
-                o[L + F1 * r] = c.y;
-                if constexpr (KM == 3) Xw[KM == 3 ? hf : 0][r] = c;
-            } else {
-                st_s(o + F1 * r, V[r].x);
-                st_s(o + L + F1 * r, V[r].y);
-            }
-        }
-        if constexpr (KM == 3) line_fft<L, false, true>(Xw[KM == 3 ? hf : 0], j, my, tw);  // F(x0) rows
-        GD_TRACE(8 + hf);
-    });
-    if constexpr (KM == 3) w1_columns<L>(a, Xw, S, nyq, nyqc, tw, g, tid);
-}
-
-// Iteration 0's W~ for the fused init (C_G_W1's arithmetic: W~ = (rho2 (|H|^2 F(x0) + 0) + G) / (1 + rho2))
-// without parking: no inverse follows, so once column A is gathered into registers, slice B's bins
-// go straight from the row FFTs' registers into S, and column A is transformed with register (DPP)
-// transposes while S holds them.  Moves x0 = zin, |H|^2, G in and W~ out (3.5 words per pixel).
-template <int L>
-__global__ __launch_bounds__(1024) void k_gal_w1(Args a) {
-    using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
-    static_assert(F1 == 16 && F2 == 16, "register transposes for 16 x 16 lines");
-    __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // line 0's split scratch, then the Nyquist column's spectrum
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
-    const bool l0 = (line == 0);
-    float2* my = S + line * FG::XCH;
-    fill_twiddles<L>(tw, tid, FG::THREADS);
-    float2 X[FG::PPL][F2];
-    {
-        const float* z = a.o2 + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
-        }
-    }
-    __syncthreads();  // twiddles
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
-    w1_columns<L>(a, X, S, nyq, nyqc, tw, g, tid);
-}
-
-// No-park variant (gd_set_fused_iteration(2)): the column transforms use the register (DPP) transpose,
-// so S can hold slice B's bins while column A is transformed, and column A's results go to S (rows of
-// the first half) or stay in registers (second half) while column B is processed.  Nothing round-trips
-// through global memory: the iteration moves exactly its algorithmic 7.5 words per pixel (k_gal_iter
-// adds 2 x 131 KiB of parked registers per galaxy, ~21 % of its fabric traffic).
-template <int L, bool FIRST, bool LAST>
-__global__ __launch_bounds__(1024) void k_gal_iter2(Args a) {
-    using FG = FusedGeo<L>;
-    constexpr int F1 = FG::F1, F2 = FG::F2, KS = FG::KS, SLD = FG::SLD, LINES = FG::LINES;
-    constexpr float inv_n = float(1.0 / double(L * L));
-    static_assert(F1 == 16 && F2 == 16, "register transpose: 16 x 16 lines");
-    __shared__ float2 tw[L];
-    __shared__ __attribute__((aligned(16))) float2 S[FG::U];
-    __shared__ float2 nyq[FG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
-    __shared__ float2 nyqx[L];      // line 0's packed column 0 / Nyquist spectrum (S holds slice B)
-    __shared__ float nyqo[L];       // x(., L/2)
-    const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
-    const bool l0 = (line == 0);
-    float2* my = S + line * FG::XCH;
-    fill_twiddles<L>(tw, tid, FG::THREADS);
-    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
-    GD_TRACE(0);
-
-    // R: pair p = line + LINES q, row FFTs with the LDS exchange (S is free)
-    float2 X[FG::PPL][F2];
-    {
-        const float* z = a.a0 + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < FG::PPL; ++q) {
-            const float* r0 = z + (size_t)(2 * (line + LINES * q)) * L + j;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) X[q][r] = make_float2(r0[F1 * r], r0[L + F1 * r]);
-        }
-    }
-    __syncthreads();  // twiddles
-    GD_TRACE(1);
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) line_fft<L, false, true>(X[q], j, my, tw);
-    lds_barrier();  // exchange areas -> slice A
-    GD_TRACE(2);
-
-    // A: bins of columns 0..KS-1 and the Nyquist bins
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        const int p = line + LINES * q;
-        float2* row = S + p * SLD;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            const int k = j + F1 * r;
-            if (r < KS / F1) row[k] = X[q][r];
-            if (r == 0 && j == 0) row[KS] = X[q][r];
-            if (r == L / 2 / F1 && j == 0) nyq[p] = X[q][r];
-            if (r > (L - KS) / F1 || (r == (L - KS) / F1 && j > 0)) row[KS + L - k] = X[q][r];
-        }
-    }
-    lds_barrier();
-    float2 C[F2];
-    fused_gather<L>(S, line, j, C);
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const int y = j + F1 * s;
-        const float2 w = nyq[y >> 1];
-        if (l0) C[s].y = (y & 1) ? w.y : w.x;
-    }
-    lds_barrier();  // slice A read -> slice B
-    GD_TRACE(3);
-    // B's bins -> S straight from the row registers (X dies here)
-#pragma unroll
-    for (int q = 0; q < FG::PPL; ++q) {
-        float2* row = S + (line + LINES * q) * SLD;
-#pragma unroll
-        for (int r = KS / F1; r <= (L - KS) / F1; ++r) {
-            const int k = j + F1 * r;
-            if (r < 2 * KS / F1) row[k - KS] = X[q][r];
-            if (r > L / 2 / F1 || (r == L / 2 / F1 && j > 0)) {
-                if (r < (L - KS) / F1 || j == 0) row[L - k] = X[q][r];
-            }
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // X dies here: keep its LDS stores ahead of column A's FFT
-    GD_TRACE(4);
-    GState pre[GD_FUSED_PRE > 0 ? GD_FUSED_PRE : 1];
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, line, j);
-
-    // column A in registers (S is occupied by slice B); columns 0 and L/2 ride together in line 0
-    line_fft<L, false, true, true>(C, opaque(j), nullptr, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqx[j + F1 * s] = C[s];
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < F2; ++s) {
-            const int ky = j + F1 * s;
-            const float2 z = C[s], zm = nyqx[(L - ky) & (L - 1)];
-            nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
-            C[s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-        }
-    }
-    lds_barrier();  // nyqc complete; slice B complete in S
-    if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64)
-        nyqc[tid] = gauss_iter_elem<L, FIRST, LAST>(a, ((size_t)g * FG::K + L / 2) * L + tid, nyqc[tid], r1, r2, r2n,
-                                                 true, inv_n);
-    fused_update<L, FIRST, LAST>(a, C, g, line, j, r1, r2, r2n, pre);
-    lds_barrier();  // Nyquist results
-#pragma unroll
-    for (int s = 0; s < F2; ++s) {
-        const float2 cn = nyqc[j + F1 * s];
-        if (l0) C[s] = make_float2(C[s].x - cn.y, C[s].y + cn.x);
-    }
-    line_fft<L, true, true, true>(C, opaque(j), nullptr, tw);
-    if (l0) {
-#pragma unroll
-        for (int s = 0; s < F2; ++s) nyqo[j + F1 * s] = C[s].y;
-    }
-    GD_TRACE(5);
-
-    // B: gather, then column A's first-half rows -> S (row layout [yl][SLD], A at [line])
-    fused_prefetch<L, FIRST, LAST>(a, pre, g, KS + line, j);
-    float2 Cb[F2];
-    fused_gather<L>(S, line, j, Cb);
-    lds_barrier();  // slice B read -> row half spectra
-    GD_TRACE(6);
-#pragma unroll
-    for (int s = 0; s < F2 / 2; ++s) {
-        float2* rr = S + (j + F1 * s) * SLD;
-        rr[line] = make_float2(C[s].x, l0 ? 0.f : C[s].y);  // column 0: real part (irfft)
-    }
-#if GD_ITER2_PARKA
-    // column A's second-half rows wait for phase I half 1 in this galaxy's output rows [L/2, L)
-    // (written only at the very end; z is fully loaded since phase R): 16 VGPRs fewer under column B
-    float2* parkA = reinterpret_cast<float2*>(a.o0 + (size_t)g * L * L + (size_t)(L / 2) * L);
-#pragma unroll
-    for (int s = F2 / 2; s < F2; ++s) parkA[(s - F2 / 2) * FG::THREADS + tid] = C[s];
-#endif
-    __builtin_amdgcn_sched_barrier(0);  // C's first half (and with GD_ITER2_PARKA all of C) dies here
-    line_fft<L, false, true, true>(Cb, opaque(j), nullptr, tw);
-    fused_update<L, FIRST, LAST>(a, Cb, g, KS + line, j, r1, r2, r2n, pre);
-    line_fft<L, true, true, true>(Cb, opaque(j), nullptr, tw);
-    GD_TRACE(7);
-
-    // I: half hf = rows [hf L/2, (hf+1) L/2): row IFFT of the packed pairs, store
-    float* out = a.o0 + (size_t)g * L * L;
-    static_for<0, 2>([&](auto hfc) {
-        constexpr int hf = decltype(hfc)::value;
-        if constexpr (hf == 1) {
-            lds_barrier();  // exchange areas -> row half spectra
-#pragma unroll
-            for (int s = F2 / 2; s < F2; ++s) {
-                float2* rr = S + (j + F1 * s - L / 2) * SLD;
-#if GD_ITER2_PARKA
-                const float2 c = parkA[(s - F2 / 2) * FG::THREADS + opaque(tid)];
-#else
-                const float2 c = C[s];
-#endif
-                rr[line] = make_float2(c.x, l0 ? 0.f : c.y);
-            }
-        }
-#pragma unroll
-        for (int s = hf * F2 / 2; s < (hf + 1) * F2 / 2; ++s) S[(j + F1 * s - hf * L / 2) * SLD + KS + line] = Cb[s];
-        for (int i = tid; i < L / 2; i += FG::THREADS) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        lds_barrier();
-        float2 V[F2];
-        {
-            const int jj = opaque(j);
-            const float2* re = S + (2 * opaque(line)) * SLD;
-            const float2* ro = re + SLD;
-#pragma unroll
-            for (int r = 0; r < F2; ++r) {
-                const int k = jj + F1 * r;
-                float2 be, bo;
-                if (k <= L / 2) {
-                    be = re[k];
-                    bo = ro[k];
-                } else {
-                    be = cconj(re[L - k]);
-                    bo = cconj(ro[L - k]);
-                }
-                V[r] = make_float2(be.x - bo.y, be.y + bo.x);
-            }
-        }
-        lds_barrier();  // row half spectra -> exchange areas
-        line_fft<L, true, true>(V, j, my, tw);
-        float* o = out + (size_t)(hf * L / 2 + 2 * line) * L + j;
-#pragma unroll
-        for (int r = 0; r < F2; ++r) {
-            o[F1 * r] = V[r].x;
-            o[L + F1 * r] = V[r].y;
-        }
-        GD_TRACE(8 + hf);
-    });
-}
-
 #include "gd_galreg.hpp"  // k_gal_reg: the 512-thread, register-resident fused iteration
 #include "gd_rlreg.hpp"   // k_rl_reg: the whole Richardson-Lucy loop per galaxy on the same skeleton
 #include "gd_poisreg.hpp" // k_pois_b: Poisson pass B (pass A is k_gal_reg<L, true>)
@@ -1648,7 +958,7 @@ __device__ __forceinline__ void small_gather(const float2* D, int j, int r, floa
 // at 128^2), so one 256-thread workgroup per galaxy runs the whole iteration on chip - row FFTs of z,
 // column FFTs + the spectral update (gauss_iter_elem, same state layout as k_col<G_ITER*>), inverse
 // column FFTs, inverse row FFTs, zin stored - in ONE launch instead of RF -> C -> RI through the
-// workspace.  Moves z, the state and zin only (the 2 img + 5.5 half of k_gal_iter).  A line's row
+// workspace.  Moves z, the state and zin only (the 2 img + 5.5 half of k_gal_reg).  A line's row
 // buffer for the post-FFT split is its own exchange area (F1 (F2 + 1) >= L + 2 for every plan).
 template <int L, bool FIRST, bool LAST>
 __global__ __launch_bounds__(256) void k_gal_small(Args a) {
@@ -1740,129 +1050,17 @@ __global__ __launch_bounds__(256) void k_gal_small(Args a) {
     GD_TRACE(4);
 }
 
-// k_gal_small on a transposing line plan (TP x TQ, more lanes per line than Plan<L>): at 48^2 the 4 x 12
-// plan puts one line on 4 lanes, so each phase is one 48-point transform per thread, a long dependent
-// chain at one wave per SIMD (the launch is one latency-bound round).  8 x 6 spreads a line over 8 lanes
-// (DFT-6 + DFT-8 per lane instead of DFT-12 + 3 DFT-4): forward transforms go (8 lanes x 6 points) ->
-// (6 lanes x 8 points) and the inverses back (tline_fft), so rows load / store and columns read / write
-// S in the 8 x 6 layout and the spectral update runs on the 6 x 8 one.  Same state, same arithmetic per
-// bin (gauss_iter_st) and the same launch contract as k_gal_small.
-#ifndef GD_SMALL_T
-#define GD_SMALL_T 2  // 1: k_gal_small_t<48> (8 x 6); 2: k_gal_small_p<48> (packed row spectra in LDS) for the 48^2 iteration
-#endif
-template <int L, int TP, int TQ, bool FIRST, bool LAST>
-__global__ __launch_bounds__(256) void k_gal_small_t(Args a) {
-    constexpr int G = TP > TQ ? TP : TQ, K = L / 2 + 1, LINES = 256 / G, XCH = TP * (TQ + 1) > TQ * (TP + 1)
-                                                                               ? TP * (TQ + 1) : TQ * (TP + 1);
-    static_assert(TP * TQ == L && G == TP && XCH >= L + 2 && L / 2 <= LINES && K <= LINES, "one line per thread");
-    constexpr float inv_n = float(1.0 / double(L * L));
-    __shared__ float2 tw[L];
-    __shared__ float2 S[K * L];  // [kx][ky]
-    __shared__ float2 xch[LINES * XCH];
-    const int tid = threadIdx.x, line = tid / G, j = tid - line * G;
-    const int g = blockIdx.x;
-    float2* my = xch + line * XCH;
-    GD_TRACE(0);
-    // z's row pair of this line, loaded first (its latency hides behind the twiddles and the prefetch)
-    const float* z = a.a0 + (size_t)g * L * L;
-    float2 v[G];
-    if (line < L / 2) {
-#pragma unroll
-        for (int s = 0; s < TQ; ++s) v[s] = make_float2(z[(2 * line) * L + j + TP * s], z[(2 * line + 1) * L + j + TP * s]);
-    }
-    fill_twiddles<L>(tw, tid, 256);
-    const float r1 = a.rho1(g), r2 = a.rho2(g), r2n = LAST ? 0.f : a.rho2n(g);
-    // the state of this line's column (6 x 8 layout: lane j < TQ holds ky = j + TQ k1), loaded now
-    GState pre[TP];
-    const bool cl = line < K && j < TQ;
-    if (cl) {
-        const size_t ob = ((size_t)g * K + line) * L + j;
-#pragma unroll
-        for (int k1 = 0; k1 < TP; ++k1) pre[k1] = gauss_load<L, FIRST, LAST>(a, ob + TQ * k1);
-    }
-    __syncthreads();
-    GD_TRACE(1);
-
-    // R: row pair -> FFT -> the two rows' half spectra into S (transposed); the spectrum leaves the
-    // transform in the 6 x 8 layout, written to the line's area in natural order for the split
-    if (line < L / 2) {
-        tline_fft<L, TP, TQ, false>(v, j, my, tw);
-        if (j < TQ) {
-#pragma unroll
-            for (int k1 = 0; k1 < TP; ++k1) my[j + TQ * k1] = v[k1];
-        }
-        wave_lds_sync();
-        const int r = 2 * line;
-        for (int k = j; k < K; k += G) {
-            const float2 C = my[k], Dm = my[k == 0 ? 0 : L - k];
-            S[k * L + r] = make_float2(0.5f * (C.x + Dm.x), 0.5f * (C.y - Dm.y));
-            S[k * L + r + 1] = make_float2(0.5f * (C.y + Dm.y), 0.5f * (Dm.x - C.x));
-        }
-        wave_lds_sync();
-    }
-    __syncthreads();  // all of z read (zin may alias z), S complete
-    GD_TRACE(2);
-
-    // C: column kx -> FFT -> spectral update (6 x 8 layout) -> IFFT (back in place, 8 x 6)
-    if (line < K) {
-        const int kx = line;
-#pragma unroll
-        for (int s = 0; s < TQ; ++s) v[s] = S[kx * L + j + TP * s];
-        tline_fft<L, TP, TQ, false>(v, j, my, tw);
-        const size_t ob = ((size_t)g * K + kx) * L + (j < TQ ? j : 0);
-#pragma unroll
-        for (int k1 = 0; k1 < TP; ++k1)
-            v[k1] = gauss_iter_st<L, FIRST, LAST>(a, ob + TQ * k1, v[k1], pre[k1], r1, r2, r2n, cl, inv_n);
-        tline_fft<L, TQ, TP, true>(v, j, my, tw);
-#pragma unroll
-        for (int s = 0; s < TQ; ++s) S[kx * L + j + TP * s] = v[s];
-    }
-    __syncthreads();
-    GD_TRACE(3);
-
-    // I: Hermitian-extended packed pair spectrum (6 x 8 layout) -> inverse row FFT -> zin (x last)
-    float* out = a.o0 + (size_t)g * L * L;
-    if (line < L / 2) {
-        const int r = 2 * line;
-        if (j < TQ) {
-#pragma unroll
-            for (int k1 = 0; k1 < TP; ++k1) {
-                const int k = j + TQ * k1;
-                const bool self = (k == 0) || (2 * k == L);
-                float2 be, bo;
-                if (2 * k <= L) {
-                    be = S[k * L + r];
-                    bo = S[k * L + r + 1];
-                } else {
-                    be = cconj(S[(L - k) * L + r]);
-                    bo = cconj(S[(L - k) * L + r + 1]);
-                }
-                if (self) {
-                    be.y = 0.f;
-                    bo.y = 0.f;
-                }
-                v[k1] = make_float2(be.x - bo.y, be.y + bo.x);
-            }
-        }
-        tline_fft<L, TQ, TP, true>(v, j, my, tw);
-#pragma unroll
-        for (int s = 0; s < TQ; ++s) {
-            out[r * L + j + TP * s] = v[s].x;
-            out[(r + 1) * L + j + TP * s] = v[s].y;
-        }
-    }
-    GD_TRACE(4);
-}
-
-// k_gal_small_t with the row pairs' PACKED spectra in LDS (GD_SMALL_T = 2): the row phase stores each pair's
+// The 48^2 iteration (k_gal_small_p<48, 8, 6>): one 256-thread workgroup per galaxy on a transposing line plan
+// (tline_fft: 8 lanes x 6 points per 48-point line, DFT-6 + DFT-8 per lane instead of the 4 x 12 plan's DFT-12 and
+// three DFT-4s), with the row pairs' PACKED spectra in LDS.  The row phase stores each pair's
 // transform as it leaves tline_fft (PR[kx][p], kx in [0, L), no split through the exchange area), the column
 // line kx reads the packed columns kx and L - kx and separates its rows' bins on the fly (the split's
 // arithmetic), and after the inverse column transform it writes the next row phase's packed input for both
 // columns kx and L - kx (the gather's Hermitian extension, bins kx = 0, L/2 real) in place - the columns
 // {kx, L - kx} belong to that line alone, so no barrier separates its reads and writes.  A lane holds rows
 // r = j + TP r' (one parity per lane): the packing pairs lanes j, j ^ 1 through a DPP quad swap.  Per line:
-// R 8 LDS stores instead of 8 + 2 syncs + ~16 split accesses, I 8 reads instead of 16; the same arithmetic
-// per bin as k_gal_small_t, so the outputs are bit-identical to it.
+// R 8 LDS stores instead of 8 + 2 syncs + ~16 split accesses, I 8 reads instead of 16 (round 4: bit-identical
+// to the retired unpacked form).
 template <int L, int TP, int TQ, bool FIRST, bool LAST>
 __global__ __launch_bounds__(256) void k_gal_small_p(Args a) {
     constexpr int G = TP > TQ ? TP : TQ, K = L / 2 + 1, LINES = 256 / G, XCH = TP * (TQ + 1) > TQ * (TP + 1)
@@ -2959,8 +2157,6 @@ constexpr const char* kPsfRowsName = "k_psf_rows";
 constexpr const char* kColName = "k_col";
 constexpr const char* kRowInvName = "k_row_inv";
 constexpr const char* kRowInvFwdName = "k_row_invfwd";
-constexpr const char* kGalIterName = "k_gal_iter";
-constexpr const char* kGalIter2Name = "k_gal_iter2";
 constexpr const char* kGalRegName = "k_gal_reg";
 constexpr const char* kGalInitName = "k_gal_init";
 constexpr const char* kGalSmallName = "k_gal_small";
@@ -3067,42 +2263,17 @@ struct Launcher {
         hipLaunchKernelGGL((k_row_inv<L, MODE>), dim3(row_grid<RiTraits<MODE>::NI>(a.N)), dim3(RowGeo<L, RiTraits<MODE>::NI>::THREADS), 0, st, a);
         return check_launch("k_row_inv");
     }
-    template <bool FIRST, bool LAST>
-    static int gal_iter_v(const Args& a, hipStream_t st) {
-        ProfScope ps(nm(kGalIterName, FIRST + 2 * LAST), st);
-        hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
-        return check_launch("k_gal_iter");
-    }
     static int psf_rows_state(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kPsfRowsName, 1), st);
         const int bpg = (a.h / 2 + G::LPB - 1) / G::LPB;
         hipLaunchKernelGGL((k_psf_rows<L, true>), dim3(a.N * bpg), dim3(256), 0, st, a);
         return check_launch("k_psf_rows");
     }
-    template <int KM>
-    static int gal_init_v(const Args& a, hipStream_t st) {
-        ProfScope ps(nm(kGalInitName, KM), st);
-        if constexpr (KM == 2) {
-            hipLaunchKernelGGL((k_gal_w1<L>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
-            return check_launch("k_gal_w1");
-        } else {
-            hipLaunchKernelGGL((k_gal_iter<L, false, false, KM>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
-            return check_launch("k_gal_iter");
-        }
-    }
-    template <bool FIRST, bool LAST>
-    static int gal_iter2_v(const Args& a, hipStream_t st) {
-        ProfScope ps(nm(kGalIter2Name, FIRST + 2 * LAST), st);
-        hipLaunchKernelGGL((k_gal_iter2<L, FIRST, LAST>), dim3(a.N), dim3(FusedGeo<L>::THREADS), 0, st, a);
-        return check_launch("k_gal_iter2");
-    }
     template <bool FIRST, bool LAST>
     static int gal_small_v(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kGalSmallName, FIRST + 2 * LAST), st);
-        if constexpr (L == 48 && GD_SMALL_T == 2)  // packed row spectra in LDS (k_gal_small_p)
+        if constexpr (L == 48)  // packed row spectra in LDS, 8 x 6 line plan (k_gal_small_p)
             hipLaunchKernelGGL((k_gal_small_p<L, 8, 6, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
-        else if constexpr (L == 48 && GD_SMALL_T)  // 8 lanes per 48-point line (k_gal_small_t)
-            hipLaunchKernelGGL((k_gal_small_t<L, 8, 6, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
         else
             hipLaunchKernelGGL((k_gal_small<L, FIRST, LAST>), dim3(a.N), dim3(256), 0, st, a);
         return check_launch("k_gal_small");
@@ -3146,15 +2317,6 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_reg_init<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_reg_init");
     }
-    static int gal_iter(const Args& a, hipStream_t st, int variant) {
-        if (variant == 1) return gal_reg(a, st);
-        if (variant == 2) {
-            if (a.first) return a.last ? gal_iter2_v<true, true>(a, st) : gal_iter2_v<true, false>(a, st);
-            return a.last ? gal_iter2_v<false, true>(a, st) : gal_iter2_v<false, false>(a, st);
-        }
-        if (a.first) return a.last ? gal_iter_v<true, true>(a, st) : gal_iter_v<true, false>(a, st);
-        return a.last ? gal_iter_v<false, true>(a, st) : gal_iter_v<false, false>(a, st);
-    }
     template <int MODE>
     static int rif(const Args& a, hipStream_t st) {
         ProfScope ps(nm(kRowInvFwdName, MODE), st);
@@ -3180,15 +2342,14 @@ struct Launcher {
 size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk; 0 = one pass
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
-int g_fused = 1;  // Gaussian iterations at 256^2: 1 = k_gal_reg, 2 = k_gal_iter2, 3 = k_gal_iter (parking); 0 = chunked
+int g_fused = 1;  // Gaussian iterations (and Poisson ones at 256^2 / L <= 112): 1 = the one-launch kernels; 0 = chained
 int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per galaxy), 0 = chunked chain
 // gd_subnet_rhos_psf: one fused launch per galaxy up to this batch (one round of workgroups on the 256 CUs:
 // 60.5 vs 75.5 us at 256 x 48^2), else the feature kernel + batched MLP (1024: 173 vs 212 us; 4096: 584 vs
 // 818 us fused - each fused workgroup re-reads the MLP weights, and 129 VGPRs allow one per CU)
 int g_subnet_fused_max = 256;
 int g_sri_map = 0;  // k_subnet_rhos_init's block -> (role, galaxy) map (tools/kbench_small)
-int g_fused_init = 1;  // Gaussian init at 256^2 (+ k_psf_rows<STATE>): 1 = k_gal_reg_init, 2 = k_gal_iter<KM = 1> +
-                       // k_gal_w1, 3 = k_gal_iter<KM = 3>; 0 = chunked
+int g_fused_init = 1;  // Gaussian init (256^2: k_psf_rows<STATE> + k_gal_reg_init) and the other one-launch inits: 1 on; 0 = chunked
 
 struct PipeRes {
     bool ok = false;
@@ -3413,11 +2574,6 @@ struct Ops {
         if constexpr (has_fused<L>()) {
             if (g_fused_init && a0.h <= 64) {  // whole-galaxy passes, no workspace: PSF rows -> U1 slot, init, W~
                 GD_TRY(Lc::psf_rows_state(a0, st0));
-                if (g_fused_init == 2) {
-                    GD_TRY(Lc::template gal_init_v<1>(a0, st0));
-                    return Lc::template gal_init_v<2>(a0, st0);
-                }
-                if (g_fused_init == 3) return Lc::template gal_init_v<3>(a0, st0);
                 return Lc::gal_reg_init(a0, st0);
             }
         }
@@ -3435,7 +2591,7 @@ struct Ops {
     static int admm_iter_gauss(Args a, hipStream_t st0) {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
         if constexpr (has_fused<L>()) {
-            if (g_fused) return Lc::gal_iter(a, st0, g_fused);  // one pass, no workspace
+            if (g_fused) return Lc::gal_reg(a, st0);  // one pass, no workspace
         }
         if constexpr (GD_MID_EXTRA && (L == 96 || L == 128)) {
             if (g_fused) return gal_mid_launch_t<L>(a, st0);  // k_gal_mid
@@ -4024,7 +3180,7 @@ int gd_set_pipeline_streams(int streams) {
 
 int gd_set_fused_init(int on) {
     const int old = g_fused_init;
-    g_fused_init = (on >= 1 && on <= 3) ? on : 0;
+    g_fused_init = on ? 1 : 0;
     return old;
 }
 
@@ -4042,7 +3198,7 @@ int gd_set_subnet_fused_max(int n) {
 
 int gd_set_fused_iteration(int on) {
     const int old = g_fused;
-    g_fused = (on >= 1 && on <= 3) ? on : 0;
+    g_fused = on ? 1 : 0;
     return old;
 }
 

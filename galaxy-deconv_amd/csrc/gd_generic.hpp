@@ -740,7 +740,8 @@ struct GOps {
     static int admm_init_gauss(Args a0, hipStream_t st0) {
         // Gaussian state |H|^2, G and iteration 0's W~; x0 -> zin (a.o2)
         // 80 / 112 / 144 / 160: one launch, one workgroup per galaxy (k_gal_mid_init: the same state as this chain)
-        if (GD_MID_FUSED && g_fused_init && mid_size(a0.gH, a0.gW) && a0.pw == 0) return gal_mid_init_launch(a0, st0);
+        // (one predicate for every mid size, compile-time 96 / 128 included: both switches on)
+        if (GD_MID_FUSED && g_fused && g_fused_init && mid_size(a0.gH, a0.gW) && a0.pw == 0) return gal_mid_init_launch(a0, st0);
         return chunks(a0, st0, [&](const Args& a, hipStream_t st) {
             Args b = a;
             GD_TRY(Lc::rf<RF_PSF_Y>(b, st));  // placed PSF -> slot 0, max(y,0)/alpha -> slot 1

@@ -88,9 +88,24 @@ def source_files():
             os.path.join(ROOT, "include", "gdeconv.h")]
 
 
+# hipcc flags of the in-tree build (__graft_entry__.build); part of the provenance hash below, so a library
+# built with other flags (offload arch, -D switches) is rebuilt and refused by smoke()
+BUILD_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result"]
+
+
+def _toolchain_id():
+    """The ROCm release the build uses (/opt/rocm/.info/version; the same image on the GPU box)."""
+    try:
+        with open("/opt/rocm/.info/version") as f:
+            return f.read().strip()
+    except OSError:
+        return "unknown"
+
+
 def source_hash():
-    """sha256 (first 16 hex digits) over the names and contents of ``source_files()``: what build() compiles
-    into the library (``gd_engine_src_hash``) and smoke() checks against the tree it runs in."""
+    """sha256 (first 16 hex digits) over the names and contents of ``source_files()``, the build flags and the
+    ROCm release: what build() compiles into the library (``gd_engine_src_hash``) and smoke() checks against the
+    tree it runs in."""
     import hashlib
     h = hashlib.sha256()
     for p in source_files():
@@ -98,6 +113,7 @@ def source_hash():
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
+    h.update(("flags:" + " ".join(BUILD_FLAGS) + "\0rocm:" + _toolchain_id()).encode())
     return h.hexdigest()[:16]
 
 

@@ -12,8 +12,10 @@
  *     contiguous); `ws` is a workspace of gd_workspace_bytes(N, H, W) bytes;
  *   - sizes: any H x W with 2 <= H, W <= 1638 (utils/utils_torch.py's torch.fft path takes any size);
  *     square 32/48/64/96/128/256 run compile-time-planned kernels, every other size the runtime-
- *     planned ones (csrc/gd_generic.hpp) with the same operation chains; PSFs square, even side
- *     <= min(H, W).
+ *     planned ones (csrc/gd_generic.hpp) with the same operation chains.  The Gaussian ADMM init and
+ *     iteration run one launch per call at 256^2 (k_gal_reg_init / k_gal_reg), 32/48/64 (k_gal_small*)
+ *     and every multiple of 16 from 80 to 160, 96 and 128 included (k_gal_mid_init / k_gal_mid); PSFs
+ *     square, even side <= min(H, W).
  *
  * Reference interfaces replaced (paths relative to mbertagna/Galaxy-Deconv @ 2025-03-07):
  *   gd_psf_to_otf       utils/utils_torch.py:79-92   psf_to_otf(ker, size)
@@ -216,11 +218,10 @@ int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride,
 size_t gd_set_chunk_bytes(size_t bytes);
 int gd_set_pipeline_streams(int streams);
 
-/* Fused Gaussian iteration: at sizes that have it (256^2) gd_admm_iter runs ONE kernel per call, one
- * workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic).  on: 1 = k_gal_reg
- * (default: 512 threads, nothing parked in global memory), 2 = k_gal_iter2, 3 = k_gal_iter (1024
- * threads, parks registers in the output image); 0 selects the three-kernel path (row pass / column
- * pass / row pass through the workspace).  Returns the previous setting; process-wide. */
+/* Fused iterations: at the sizes that have them (see "sizes" above; Poisson at 256^2 and square L <= 112)
+ * gd_admm_iter runs one workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic).
+ * on != 0 (default 1) selects them; 0 selects the chained path (row pass / column pass / row pass through
+ * the workspace).  Returns the previous setting (0 or 1); process-wide. */
 int gd_set_fused_iteration(int on);
 
 /* Richardson-Lucy at 256^2 (gd_richardson_lucy, models/Richard_Lucy.py:10-24): on = 1 (default) runs the
@@ -240,12 +241,11 @@ int gd_set_subnet_fused_max(int n);
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->
- * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic.  on: 1 = k_gal_reg_init
- * (default, one launch), 2 = k_gal_iter<KM=1> + k_gal_w1 (two launches), 3 = k_gal_iter<KM=3> (one
- * launch, 1024 threads); 0 selects the chunked chain.  At 160^2 any non-zero value selects k_gal_mid_init
- * (one launch: the placed PSF's row spectra parked in the U1 slot, the half spectrum in LDS) in place of
- * the runtime-planned RF_PSF_Y -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain.  Returns the previous setting;
- * process-wide. */
+ * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic (k_gal_reg_init).  on != 0
+ * (default 1) selects it, 0 the chunked chain.  At the mid sizes (80 ... 160, multiples of 16) the one-launch
+ * k_gal_mid_init (the placed PSF's row spectra parked in the U1 slot, the half spectrum in LDS) runs when
+ * BOTH this and gd_set_fused_iteration are on, in place of the RF_PSF_Y -> C_G_INIT -> RIF_CLAMP -> C_G_W1
+ * chain.  Returns the previous setting (0 or 1); process-wide. */
 int gd_set_fused_init(int on);
 
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,

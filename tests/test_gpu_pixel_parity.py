@@ -31,7 +31,7 @@ import pytest
 import torch
 
 import admm_oracle as O
-from conftest import golden
+from conftest import golden, parity_gate
 
 pytestmark = pytest.mark.gpu
 
@@ -86,10 +86,9 @@ def check(tag, out, gold, ref64):
     if log:
         with open(log, "a") as f:
             f.write(json.dumps(rec) + "\n")
-    # engine-limited (conftest.parity_gate): the engine's own error, and its agreement with the reference
-    # up to the reference's own distance from the exact result
-    assert rec["engine_vs_fp64_normwise"] < TOL, rec
-    assert rec["engine_vs_reference_normwise"] < TOL + rec["reference_vs_fp64_normwise"], rec
+    # the normwise gate, per galaxy (conftest.parity_gate): engine vs fp64 <= 1e-5 and engine vs the
+    # reference <= 1e-5, relaxed only for the listed ill-conditioned cases
+    rec["gate"] = parity_gate(tag, out, gold, ref64, tol=TOL)
     for i in (1, 2):   # p99, 32nd-largest
         assert qe[i] <= BOUND * qr[i], rec
     return rec

@@ -1,9 +1,8 @@
-// Standalone check + timing of the fused Gaussian iteration variants at 256^2 (no torch):
-// k_gal_iter (1024 threads, parking) against k_gal_reg (512 threads, no parking); both use the
-// engine's 256^2 state layout (sidx_c / sidx_h).  Both run
-// the same arithmetic in the same order; the compiler contracts multiply-adds differently in the two
-// kernels, so results agree to rounding (max |d| <= 1e-6 max |x| over zin and the U1 / W~ state is the
-// bar; the tool exits non-zero otherwise).  Then each variant is timed over the batch.
+// Standalone check + timing of the fused Gaussian iteration k_gal_reg<256> (no torch): checked against the
+// engine's chained three-kernel path (Ops<256>::admm_iter_gauss with g_fused = 0: RF_ONE -> C_G_ITER* -> RI_OUT1
+// through the workspace) on the same 256^2 state layout (sidx_c / sidx_h).  The per-bin arithmetic is the same
+// (gauss_math_rt); the transforms' rounding differs, so results agree to rounding (max |d| <= 1e-6 max |x| over
+// zin and the U1 / W~ state is the bar; the tool exits non-zero otherwise).  Then k_gal_reg is timed over the batch.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/kbench_reg tools/kbench_reg.hip
 //   tools/kbench_reg [N=4096] [reps=20] [noparity]  (noparity: time layout experiments that break the comparison)
 #include "../galaxy-deconv_amd/csrc/gd_engine.hip"
@@ -39,6 +38,7 @@ constexpr int L = 256, K = L / 2 + 1;
 struct Bufs {
     float *z, *zin;
     float2* state;  // |H|^2 (K L floats, padded to K L float2) | G | U1 | W~
+    float2* ws;     // the chained path's workspace
     Args a;
 };
 
@@ -47,7 +47,9 @@ Bufs make(int N, float* par) {
     Bufs b;
     CK(hipMalloc(&b.z, img * 4)); CK(hipMalloc(&b.zin, img * 4));
     CK(hipMalloc(&b.state, 4 * spec * 8));
+    CK(hipMalloc(&b.ws, 2 * spec * 8));
     memset(&b.a, 0, sizeof(b.a));
+    b.a.T = b.ws;
     b.a.N = N; b.a.s_hh = (float*)b.state; b.a.s_g = b.state + spec; b.a.s_u1 = b.a.s_g + spec; b.a.s_w = b.a.s_u1 + spec;
     b.a.a0 = b.z; b.a.o0 = b.zin;
     b.a.alpha = b.a.rho1 = b.a.rho2 = b.a.rho2n = GalScalar{par, 1};
@@ -87,21 +89,17 @@ __global__ __launch_bounds__(T) void k_stream(Args a) {
     }
 }
 
-template <bool FIRST, bool LAST>
-void launch(int variant, Args a) {
-    a.first = FIRST;
-    a.last = LAST;
-    if (variant == 0)
-        hipLaunchKernelGGL((k_gal_iter<L, FIRST, LAST>), dim3(a.N), dim3(1024), 0, 0, a);
-    else
+// variant 0: the chained three-kernel path (the reference), 1: k_gal_reg; fl: 0 MID, 1 FIRST, 2 LAST, 3 FIRST_LAST
+void launch_v(int variant, int fl, Args a) {
+    a.first = fl & 1;
+    a.last = fl >> 1;
+    if (variant == 0) {
+        const int old = g_fused;
+        g_fused = 0;
+        if (Ops<L>::admm_iter_gauss(a, 0) != GD_OK) { printf("chain failed: %s\n", g_last_error.c_str()); exit(1); }
+        g_fused = old;
+    } else {
         hipLaunchKernelGGL((k_gal_reg<L>), dim3(a.N), dim3(512), 0, 0, a);
-}
-void launch_v(int variant, int fl, const Args& a) {
-    switch (fl) {
-        case 0: launch<false, false>(variant, a); break;
-        case 1: launch<true, false>(variant, a); break;
-        case 2: launch<false, true>(variant, a); break;
-        default: launch<true, true>(variant, a); break;
     }
 }
 
@@ -149,7 +147,7 @@ int main(int argc, char** argv) {
         bad += !(dz <= 1e-6) || !(ds <= 1e-6);
     }
     if (bad && !(argc > 3 && !strcmp(argv[3], "noparity"))) {
-        printf("FAIL: k_gal_reg differs from k_gal_iter\n");
+        printf("FAIL: k_gal_reg differs from the chained path\n");
         return 1;
     }
     Bufs t = make(N, par);
@@ -164,13 +162,11 @@ int main(int argc, char** argv) {
         printf("k_stream<512>  (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m5, gb[0] / m5);
         printf("k_stream<1024> (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m10, gb[0] / m10);
     }
-    for (int fl = 0; fl < 3; ++fl)
-        for (int v = 0; v < 2; ++v) {
-            const float ms = time_ms([&] { launch_v(v, fl, t.a); }, reps);
-            CK(hipGetLastError());
-            printf("%-11s<256,%-5s> N=%d  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", v ? "k_gal_reg" : "k_gal_iter",
-                   fln[fl], N, ms, gb[fl] / ms, gb[fl]);
-        }
+    for (int fl = 0; fl < 3; ++fl) {
+        const float ms = time_ms([&] { launch_v(1, fl, t.a); }, reps);
+        CK(hipGetLastError());
+        printf("k_gal_reg<256,%-5s> N=%d  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", fln[fl], N, ms, gb[fl] / ms, gb[fl]);
+    }
 #if GD_FUSED_TRACE
     // per-phase durations of k_gal_reg<MID> (thread 0's s_memrealtime stamps, 100 MHz) at several batch sizes
     const char* names[] = {"start -> z loaded", "row FFTs", "slice A -> S + gather", "column A FFT + update",

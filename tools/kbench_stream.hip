@@ -1,116 +1,245 @@
-// Streaming ceiling of the fused iteration's per-galaxy byte mix (z, |H|^2, G, U1, W~ in; U1, W~, zin out:
-// 1,977,344 B per galaxy at 256^2) for one workgroup per CU (LDS padded like k_gal_reg), as a function of
-// the 16-byte loads each thread keeps in flight (U) and the workgroup size (T), and for a pure copy.
+// Streaming ceilings on MI355X (round 5 rewrite).  Two questions:
+//  (1) what a plain HBM stream reaches with this build and this box: copy / read-only / write-only, 16-byte
+//      accesses per lane, workgroup size T, loads in flight per thread U, grid (persistent multiples of the CU
+//      count or one pass over the data), default or non-temporal (nt) loads and stores, random data;
+//  (2) what the fused 256^2 iteration's per-galaxy byte mix reaches (z, |H|^2, G, U1, W~ in; U1, W~, zin out:
+//      1,977,344 B per galaxy, 2 img + 5.5 half spectra), one workgroup per galaxy with k_gal_reg's LDS
+//      footprint (one workgroup per CU), for the state in the engine's layout (four arrays, SoA) and in an
+//      interleaved layout (a column's |H|^2, G, U1, W~ in one contiguous record, AoS), with the z read and
+//      zin write either in their own phases (as k_gal_reg: z first, zin last) or spread over the galaxy.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/kbench_stream tools/kbench_stream.hip
+//   tools/kbench_stream [N=4096] [reps=20]
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int L = 256, K = L / 2 + 1;
 constexpr size_t IMG = (size_t)L * L, SPEC = (size_t)K * L;
 
-template <int T, int U, bool NT>
-__global__ __launch_bounds__(T) void k_mix(const float* z, float* zin, const float* hh, const float2* G, float2* Uu,
-                                           float2* W, int N) {
-    __shared__ float pad[35000];
-    if (threadIdx.x == 0) pad[0] = 0.f;
-    for (int g = blockIdx.x; g < N; g += gridDim.x) {
-        const f4v* zs = reinterpret_cast<const f4v*>(z + g * IMG);
-        f4v* zo = reinterpret_cast<f4v*>(zin + g * IMG);
-        constexpr int NZ = IMG / 4;
-        static_assert(NZ % (T * U) == 0, "image loop is exact");
-        for (int i0 = threadIdx.x; i0 < NZ; i0 += T * U) {
-            f4v v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = zs[i0 + u * T];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (NT) __builtin_nontemporal_store(v[u] * 1.5f, zo + i0 + u * T);
-                else zo[i0 + u * T] = v[u] * 1.5f;
-            }
-        }
-        const f4v* h4 = reinterpret_cast<const f4v*>(hh + g * SPEC);
-        const f4v* g4 = reinterpret_cast<const f4v*>(G + g * SPEC);
-        f4v* u4 = reinterpret_cast<f4v*>(Uu + g * SPEC);
-        f4v* w4 = reinterpret_cast<f4v*>(W + g * SPEC);
-        constexpr int NS = SPEC / 4;  // 4-bin groups: 1 f4v of |H|^2, 2 f4v each of G, U1, W~
-        constexpr int UU = U / 4 > 0 ? U / 4 : 1;
-        for (int i0 = threadIdx.x; i0 < NS; i0 += T * UU) {
-            f4v h[UU], gg[UU][2], uu[UU][2], ww[UU][2];
-#pragma unroll
-            for (int u = 0; u < UU; ++u) {
-                const int i = i0 + u * T < NS ? i0 + u * T : NS - 1;  // clamped: the tail re-reads, no write below
-                h[u] = h4[i];
-                gg[u][0] = g4[2 * i]; gg[u][1] = g4[2 * i + 1];
-                uu[u][0] = u4[2 * i]; uu[u][1] = u4[2 * i + 1];
-                ww[u][0] = w4[2 * i]; ww[u][1] = w4[2 * i + 1];
-            }
-#pragma unroll
-            for (int u = 0; u < UU; ++u) {
-                const int i = i0 + u * T;
-                if (i >= NS) break;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const f4v a = uu[u][e] + gg[u][e] * h[u].x, b = ww[u][e] - gg[u][e];
-                    if (NT) { __builtin_nontemporal_store(a, u4 + 2 * i + e); __builtin_nontemporal_store(b, w4 + 2 * i + e); }
-                    else { u4[2 * i + e] = a; w4[2 * i + e] = b; }
-                }
-            }
-        }
+__global__ void k_fill(float* p, size_t n, unsigned seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u + seed;
+        x ^= x >> 13; x *= 0x5bd1e995; x ^= x >> 15;
+        p[i] = (x & 0xffffff) / float(0x1000000);
     }
 }
-template <int T, int U>
+
+template <bool NT>
+__device__ __forceinline__ f4v ld(const f4v* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(f4v* p, f4v v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// ---- (1) plain streams, grid-stride over n float4
+template <int T, int U, bool NTL, bool NTS>
 __global__ __launch_bounds__(T) void k_copy(const f4v* a, f4v* b, size_t n) {
     for (size_t i0 = (size_t)blockIdx.x * T * U + threadIdx.x; i0 < n; i0 += (size_t)gridDim.x * T * U) {
         f4v v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = i0 + u * T < n ? a[i0 + u * T] : f4v{0, 0, 0, 0};
+        for (int u = 0; u < U; ++u) v[u] = i0 + u * T < n ? ld<NTL>(a + i0 + u * T) : f4v{0, 0, 0, 0};
 #pragma unroll
-        for (int u = 0; u < U; ++u) if (i0 + u * T < n) b[i0 + u * T] = v[u] + 1.f;
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * T < n) st<NTS>(b + i0 + u * T, v[u] + 1.f);
+    }
+}
+template <int T, int U, bool NTL>
+__global__ __launch_bounds__(T) void k_read(const f4v* a, f4v* sink, size_t n) {
+    f4v acc = {0, 0, 0, 0};
+    for (size_t i0 = (size_t)blockIdx.x * T * U + threadIdx.x; i0 < n; i0 += (size_t)gridDim.x * T * U) {
+        f4v v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = i0 + u * T < n ? ld<NTL>(a + i0 + u * T) : f4v{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    if (acc.x == -1.f) sink[threadIdx.x] = acc;  // never true on the [0, 1) data: keeps the loads
+}
+template <int T, int U, bool NTS>
+__global__ __launch_bounds__(T) void k_write(f4v* b, size_t n) {
+    const f4v v = {1.f, 2.f, 3.f, (float)threadIdx.x};
+    for (size_t i0 = (size_t)blockIdx.x * T * U + threadIdx.x; i0 < n; i0 += (size_t)gridDim.x * T * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * T < n) st<NTS>(b + i0 + u * T, v);
     }
 }
 
+// ---- (2) the fused iteration's byte mix, one 512-thread workgroup per galaxy, k_gal_reg's LDS footprint.
+// SoA: |H|^2 [N][K L] floats, G / U1 / W~ [N][K L] float2 (the engine's layout).
+// AoS: per galaxy and 4-bin group b (b < K L / 4) one 112-byte record {|H|^2 x4, G x4, U1 x4, W~ x4}
+//      = 7 float4; U1 / W~ rewritten in place.
+// PH = 1: z loaded before the state, zin stored after it (k_gal_reg's phase order); PH = 0: interleaved.
+template <bool AOS, bool NTS, int D>
+__device__ __forceinline__ void mix_state(const f4v* hh, const f4v* G, f4v* Uu, f4v* W, f4v* rec, int tid) {
+    constexpr int NS = SPEC / 4;  // 4-bin groups per galaxy
+    constexpr int T = 512;
+    static_assert(NS % T == 64, "tail");
+    for (int i0 = tid; i0 < NS; i0 += T * D) {
+        f4v h[D], g0[D], g1[D], u0[D], u1[D], w0[D], w1[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int i = min(i0 + d * T, NS - 1);
+            if constexpr (AOS) {
+                const f4v* r = rec + (size_t)i * 7;
+                h[d] = r[0]; g0[d] = r[1]; g1[d] = r[2]; u0[d] = r[3]; u1[d] = r[4]; w0[d] = r[5]; w1[d] = r[6];
+            } else {
+                h[d] = hh[i]; g0[d] = G[2 * i]; g1[d] = G[2 * i + 1];
+                u0[d] = Uu[2 * i]; u1[d] = Uu[2 * i + 1]; w0[d] = W[2 * i]; w1[d] = W[2 * i + 1];
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int i = i0 + d * T;
+            if (i >= NS) break;
+            const f4v a0 = u0[d] + g0[d] * h[d].x, a1 = u1[d] + g1[d] * h[d].y, b0 = w0[d] - g0[d], b1 = w1[d] - g1[d];
+            if constexpr (AOS) {
+                f4v* r = rec + (size_t)i * 7;
+                st<NTS>(r + 3, a0); st<NTS>(r + 4, a1); st<NTS>(r + 5, b0); st<NTS>(r + 6, b1);
+            } else {
+                st<NTS>(Uu + 2 * i, a0); st<NTS>(Uu + 2 * i + 1, a1); st<NTS>(W + 2 * i, b0); st<NTS>(W + 2 * i + 1, b1);
+            }
+        }
+    }
+}
+template <bool AOS, bool NTS, int D, bool PH>
+__global__ __launch_bounds__(512) void k_mix(const float* z, float* zin, const float* hh, const float2* G, float2* Uu,
+                                             float2* W, float* rec, int N) {
+    __shared__ float pad[36000];  // 144 KB: one workgroup per CU, as k_gal_reg
+    const int g = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) pad[g & 1023] = 0.f;
+    const f4v* zs = reinterpret_cast<const f4v*>(z + g * IMG);
+    f4v* zo = reinterpret_cast<f4v*>(zin + g * IMG);
+    const f4v* h4 = reinterpret_cast<const f4v*>(hh + g * SPEC);
+    const f4v* g4 = reinterpret_cast<const f4v*>(G + g * SPEC);
+    f4v* u4 = reinterpret_cast<f4v*>(Uu + g * SPEC);
+    f4v* w4 = reinterpret_cast<f4v*>(W + g * SPEC);
+    f4v* r4 = reinterpret_cast<f4v*>(rec + g * SPEC * 7);
+    constexpr int NZ = IMG / 4, PER = NZ / 512;  // 32 float4 per thread
+    if constexpr (PH) {
+        f4v v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) v[u] = zs[tid + 512 * u];
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) s += v[u].x + v[u].w;
+        pad[tid] = s;  // "row FFTs"
+        mix_state<AOS, NTS, D>(h4, g4, u4, w4, r4, tid);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; ++u) st<NTS>(zo + tid + 512 * u, v[u] * pad[(tid + u) & 511]);
+    } else {
+        for (int u0 = 0; u0 < PER; u0 += 8) {
+            f4v v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = zs[tid + 512 * (u0 + u)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) st<NTS>(zo + tid + 512 * (u0 + u), v[u] * 1.5f);
+        }
+        mix_state<AOS, NTS, D>(h4, g4, u4, w4, r4, tid);
+    }
+}
+
+// ---- timing: median of 5 timed blocks of reps launches each
 template <typename F>
 float time_ms(F&& f, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     f(); CK(hipDeviceSynchronize());
-    CK(hipEventRecord(a));
-    for (int i = 0; i < reps; ++i) f();
-    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
-    float ms; CK(hipEventElapsedTime(&ms, a, b));
-    return ms / reps;
+    std::vector<float> v;
+    for (int k = 0; k < 5; ++k) {
+        CK(hipEventRecord(a));
+        for (int i = 0; i < reps; ++i) f();
+        CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b));
+        v.push_back(ms / reps);
+    }
+    std::sort(v.begin(), v.end());
+    CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
+    return v[2];
 }
 
 int main(int argc, char** argv) {
-    const int N = argc > 1 ? atoi(argv[1]) : 4096, reps = 20;
-    float *z, *zin, *hh; float2 *G, *Uu, *W;
-    CK(hipMalloc(&z, N * IMG * 4)); CK(hipMalloc(&zin, N * IMG * 4)); CK(hipMalloc(&hh, N * SPEC * 4));
-    CK(hipMalloc(&G, N * SPEC * 8)); CK(hipMalloc(&Uu, N * SPEC * 8)); CK(hipMalloc(&W, N * SPEC * 8));
-    CK(hipMemset(z, 0, N * IMG * 4)); CK(hipMemset(hh, 0, N * SPEC * 4)); CK(hipMemset(G, 0, N * SPEC * 8));
-    CK(hipMemset(Uu, 0, N * SPEC * 8)); CK(hipMemset(W, 0, N * SPEC * 8));
-    int cus = 0; CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    const double gb = N * (2.0 * IMG * 4 + 5.5 * SPEC * 8) / 1e9;
-#define RUN(T, U, NT, grid)                                                                               \
-    {                                                                                                     \
-        const float ms = time_ms([&] { hipLaunchKernelGGL((k_mix<T, U, NT>), dim3(grid), dim3(T), 0, 0, z, zin, hh, G, Uu, W, N); }, reps); \
-        CK(hipGetLastError());                                                                           \
-        printf("mix T=%4d U=%2d nt=%d grid=%5d  %.3f ms  %.2f TB/s\n", T, U, NT, grid, ms, gb / ms);        \
-    }
-    RUN(512, 4, false, N) RUN(512, 8, false, N) RUN(512, 16, false, N)
-    RUN(512, 4, false, cus) RUN(512, 8, false, cus) RUN(512, 16, false, cus)
-    RUN(512, 8, true, cus) RUN(512, 16, true, cus)
-    RUN(1024, 8, false, cus) RUN(1024, 16, false, cus)
-    RUN(256, 16, false, cus)
+    const int N = argc > 1 ? atoi(argv[1]) : 4096, reps = argc > 2 ? atoi(argv[2]) : 20;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    // (1) plain streams over 4 GiB per buffer
     {
-        const size_t n = N * IMG / 4 * 4;  // 4 images' worth
-        f4v *a, *b;
-        CK(hipMalloc(&a, n * 16)); CK(hipMalloc(&b, n * 16)); CK(hipMemset(a, 0, n * 16));
-        for (int grid : {cus, cus * 4, 8192}) {
-            const float ms = time_ms([&] { hipLaunchKernelGGL((k_copy<256, 8>), dim3(grid), dim3(256), 0, 0, a, b, n); }, reps);
-            printf("copy T=256 U=8 grid=%5d  %.3f ms  %.2f TB/s (read+write)\n", grid, ms, 2.0 * n * 16 / 1e9 / ms);
-        }
+        const size_t n = (size_t)1 << 28;  // float4 = 4 GiB
+        f4v *a, *b, *sink;
+        CK(hipMalloc(&a, n * 16)); CK(hipMalloc(&b, n * 16)); CK(hipMalloc(&sink, 1 << 16));
+        hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, (float*)a, n * 4, 1u);
+        hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, (float*)b, n * 4, 2u);
+        CK(hipDeviceSynchronize());
+        const double gb1 = n * 16 / 1e9;
+#define COPY(T, U, NTL, NTS, grid)                                                                                   \
+    {                                                                                                                \
+        const int gr = (grid) > 0 ? (grid) : (int)((n + (size_t)T * U - 1) / ((size_t)T * U));                       \
+        const float ms = time_ms([&] { hipLaunchKernelGGL((k_copy<T, U, NTL, NTS>), dim3(gr), dim3(T), 0, 0, a, b, n); }, reps); \
+        CK(hipGetLastError());                                                                                       \
+        printf("copy  T=%4d U=%2d ntl=%d nts=%d grid=%7d  %.3f ms  %.3f TB/s (read+write)\n", T, U, NTL, NTS, gr, ms, 2 * gb1 / ms); \
+    }
+#define READ(T, U, NTL, grid)                                                                                        \
+    {                                                                                                                \
+        const int gr = (grid) > 0 ? (grid) : (int)((n + (size_t)T * U - 1) / ((size_t)T * U));                       \
+        const float ms = time_ms([&] { hipLaunchKernelGGL((k_read<T, U, NTL>), dim3(gr), dim3(T), 0, 0, a, sink, n); }, reps); \
+        CK(hipGetLastError());                                                                                       \
+        printf("read  T=%4d U=%2d ntl=%d       grid=%7d  %.3f ms  %.3f TB/s\n", T, U, NTL, gr, ms, gb1 / ms);      \
+    }
+#define WRITE(T, U, NTS, grid)                                                                                       \
+    {                                                                                                                \
+        const int gr = (grid) > 0 ? (grid) : (int)((n + (size_t)T * U - 1) / ((size_t)T * U));                       \
+        const float ms = time_ms([&] { hipLaunchKernelGGL((k_write<T, U, NTS>), dim3(gr), dim3(T), 0, 0, b, n); }, reps); \
+        CK(hipGetLastError());                                                                                       \
+        printf("write T=%4d U=%2d       nts=%d grid=%7d  %.3f ms  %.3f TB/s\n", T, U, NTS, gr, ms, gb1 / ms);      \
+    }
+        const int r1 = reps / 4 > 2 ? reps / 4 : 2;
+        (void)r1;
+        COPY(256, 4, false, false, 0) COPY(256, 8, false, false, 0) COPY(256, 16, false, false, 0)
+        COPY(512, 4, false, false, 0) COPY(1024, 4, false, false, 0)
+        COPY(256, 4, false, false, cus) COPY(256, 8, false, false, cus) COPY(256, 8, false, false, 2 * cus)
+        COPY(256, 8, false, false, 4 * cus) COPY(256, 8, false, false, 8 * cus) COPY(512, 8, false, false, 4 * cus)
+        COPY(1024, 8, false, false, 2 * cus) COPY(1024, 16, false, false, cus)
+        COPY(256, 4, false, true, 0) COPY(256, 8, false, true, 0) COPY(256, 8, false, true, 4 * cus)
+        COPY(256, 4, true, true, 0) COPY(256, 8, true, true, 4 * cus) COPY(256, 4, true, false, 0)
+        READ(256, 4, false, 0) READ(256, 8, false, 0) READ(256, 8, false, 4 * cus) READ(512, 8, false, 4 * cus)
+        READ(256, 16, false, 2 * cus) READ(256, 8, true, 0) READ(256, 8, true, 4 * cus)
+        WRITE(256, 4, false, 0) WRITE(256, 8, false, 0) WRITE(256, 8, false, 4 * cus) WRITE(256, 4, true, 0)
+        WRITE(256, 8, true, 4 * cus)
+        CK(hipFree(a)); CK(hipFree(b)); CK(hipFree(sink));
+    }
+    // (2) the fused iteration's byte mix
+    {
+        float *z, *zin, *hh, *rec;
+        float2 *G, *Uu, *W;
+        CK(hipMalloc(&z, N * IMG * 4)); CK(hipMalloc(&zin, N * IMG * 4)); CK(hipMalloc(&hh, N * SPEC * 4));
+        CK(hipMalloc(&G, N * SPEC * 8)); CK(hipMalloc(&Uu, N * SPEC * 8)); CK(hipMalloc(&W, N * SPEC * 8));
+        CK(hipMalloc(&rec, N * SPEC * 7 * 4 + 64));
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, z, N * IMG, 3u);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, hh, N * SPEC, 4u);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (float*)G, N * SPEC * 2, 5u);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (float*)Uu, N * SPEC * 2, 6u);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (float*)W, N * SPEC * 2, 7u);
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, rec, N * SPEC * 7, 8u);
+        CK(hipDeviceSynchronize());
+        const double gb = N * (2.0 * IMG * 4 + 5.5 * SPEC * 8) / 1e9;
+#define MIX(AOS, NTS, D, PH)                                                                                         \
+    {                                                                                                                \
+        const float ms = time_ms([&] { hipLaunchKernelGGL((k_mix<AOS, NTS, D, PH>), dim3(N), dim3(512), 0, 0, z, zin, hh, G, Uu, W, rec, N); }, reps); \
+        CK(hipGetLastError());                                                                                       \
+        printf("mix aos=%d nts=%d D=%d phased=%d N=%d  %.3f ms  %.3f TB/s (%.3f GB)\n", AOS, NTS, D, PH, N, ms, gb / ms, gb); \
+    }
+        MIX(false, false, 1, true) MIX(false, false, 2, true) MIX(false, false, 4, true)
+        MIX(false, true, 1, true) MIX(false, true, 2, true) MIX(false, true, 4, true)
+        MIX(true, false, 2, true) MIX(true, true, 1, true) MIX(true, true, 2, true) MIX(true, true, 4, true)
+        MIX(false, true, 2, false) MIX(true, true, 2, false)
     }
     return 0;
 }
