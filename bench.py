@@ -98,7 +98,8 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         at 256^2 reads G to form W~1, 2.5); three-kernel: + the RF / C / RI workspace round trips.
       op_admm_init, Gaussian, fused: y + PSF in, |H|^2, G, W~ (or F(x0)) + zin out = 2 img + 2.5 half
         + the PSF (h^2 floats) and at 256^2 its compact row spectra (h (L/2 + 1) complex, written and read; at
-        160^2 the packed row-pair spectra, h/2 x L complex)."""
+        160^2 the packed row-pair spectra, h/2 x L complex).
+      op_admm_init, Poisson, 256^2 two-pass: 4 img + 5 half + the PSF and its compact rows (below)."""
     img, half, n = L * L * 4, (L // 2 + 1) * L * 8, max(1, n_iters)
     k = pretty(name)
     if k == f"op_richardson_lucy<{L}>":
@@ -117,6 +118,12 @@ def op_bytes(name, L, n_iters, fused=False, h=48):
         # (160^2, k_gal_mid_init: the PSF's packed row-pair spectra [L][h/2] parked in the U1 slot, written and read)
         rows = 2 * h * (L // 2 + 1) * 8 if L == 256 else (2 * (h // 2) * L * 8 if L in (80, 96, 112, 128, 144, 160) else 0)
         return 2 * img + 2.5 * half + 4 * h * h + rows
+    if k == f"op_admm_init<{L},Poisson>" and fused and L == 256:
+        # two-pass Poisson init: k_psf_rows<STATE> (the PSF in, its compact row spectra out), k_gal_reg_init<POIS>
+        # (y, the rows in; H -> G slot, zin out, H F(x0) -> W slot, H re-read for that product: 2 img + 3 half),
+        # k_pois_b<INIT> (H F(x0), y in; w1 out, F(w1) -> W slot: 2 img + 2 half)
+        rows = 2 * h * (L // 2 + 1) * 8
+        return 4 * img + 5 * half + 4 * h * h + rows
     if k == f"op_admm_iter<{L},Poisson>":
         if fused and L == 256:
             # two-pass (gd_poisreg.hpp): pass A z, H, U1, W in, U1, H X, zin out (2 img + 5 half; first 4: no
@@ -219,6 +226,11 @@ class RLForward(torch.nn.Module):
 
     def forward(self, y, psf, alpha=None):
         return self.rl(y, psf)
+
+
+def progress(msg):
+    """A progress line on stderr (the JSON result goes to stdout alone)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def parse():
@@ -448,6 +460,7 @@ def measure(args, ctx):
     def step():
         return model(obs, psf, alpha)
 
+    progress(f"{args.workload} {N} x {L}^2 n_iters={n}: warm-up")
     with torch.no_grad():
         for _ in range(args.warmup):
             out = step()
@@ -489,6 +502,7 @@ def measure(args, ctx):
         _lib.profile_enable(0)
         kstats = _lib.profile_collect()
 
+    progress(f"timed region {(t1 - t0) * 1e3:.1f} ms for {args.steps} steps; profiling pass {tp * 1e3:.1f} ms")
     rank_times = all_ranks(t1 - t0, world, backend, dev)
     elapsed = max(rank_times)
     gal_s = N * world * args.steps / elapsed
@@ -526,6 +540,7 @@ def measure(args, ctx):
     # pays once host launch overhead is gone (matters at 48^2; reported beside value, not as value)
     graphed = None
     if not args.no_graph:
+        progress("hipGraph capture and interleaved eager / replayed blocks")
         from gdeconv.graphs import GraphedForward
         gf = GraphedForward(model, obs, psf, alpha)
         gout = gf.replay()
@@ -561,6 +576,7 @@ def measure(args, ctx):
     # the PCIe-inclusive rate from a file in the page cache (reported beside value, never as value)
     ingest = None
     if not args.no_ingest:
+        progress("packed-file ingest pipeline")
         import tempfile
         from gdeconv.ingest import DeviceBatches, PackedGalaxies, write_pack
         idir = args.ingest_dir or tempfile.gettempdir()
@@ -730,6 +746,7 @@ def measure(args, ctx):
     if rank == 0 and world == 1 and not args.no_e2e and not rl:
         # the whole model with the ResUNet denoiser (PyTorch fp32, MIOpen, NHWC) on a sample, micro-batched
         # by the model; priced against the fp32 MFMA peak (the denoiser's convolutions dominate)
+        progress("end to end with the ResUNet denoiser")
         model.Z = denoiser
         G = min(args.e2e_sample, N)
         o2, p2, a2 = obs[:G].contiguous(), psf[:G].contiguous(), alpha[:G].contiguous()
@@ -753,6 +770,7 @@ def measure(args, ctx):
     if world > 1:
         dist.barrier()   # every rank's GPU work and collectives are done before rank 0 loads the host cores
     if rank == 0 and not args.no_cpu_baseline:
+        progress("CPU baseline (the oracle on the host cores)")
         rec["cpu_baseline"] = cpu_baseline(args)
         if world > 1:
             rec["cpu_baseline"]["note"] = "rank 0, after every rank's timed and collective work"

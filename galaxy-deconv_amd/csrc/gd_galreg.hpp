@@ -68,12 +68,71 @@ __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" :
 __device__ __forceinline__ int soff_c(int kx, int m, int j) { return kx * 256 + 32 * m + 2 * j; }  // bins j + 16 (2m + e)
 __device__ __forceinline__ int soff_h(int kx, int q, int j) { return kx * 256 + 64 * q + 4 * j; }  // bins j + 16 (4q + e)
 __device__ __forceinline__ f4v ld4v(const void* p) { return *reinterpret_cast<const f4v*>(p); }
+#ifndef GD_REG_NTL
+#define GD_REG_NTL 0  // 1: the iteration's state loads non-temporal
+#endif
+__device__ __forceinline__ f4v ld4s(const void* p) {
+#if GD_REG_NTL
+    return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+#else
+    return *reinterpret_cast<const f4v*>(p);
+#endif
+}
 __device__ __forceinline__ void st4v(void* p, f4v v) {
 #if GD_NT_ST
     __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
 #else
     *reinterpret_cast<f4v*>(p) = v;
 #endif
+}
+
+// ---- 16-byte image accesses staged through the line's LDS exchange area (GD_REG_Z16).  The line FFTs want lane j
+// of a line to hold x[j + 16 r] of the pair's two rows (4-byte accesses: 64 B per line and wave instruction, each
+// 128-B line touched by two instructions).  Instead a lane loads (stores) 16 B at columns 4 j + 64 c, c < 4, of each
+// row - 256 contiguous bytes per line and instruction, a quarter of the instructions - and the values move to (from)
+// the FFT layout through the line's exchange area (272 float2 >= the pair's 256 columns, (row 2p, row 2p + 1)
+// interleaved per column: two ds_write_b128 per float4 pair, ds_read_b64 per register).  The kbench_stream pattern
+// test put the 4-byte form at 5.42 TB/s and the 16-byte one at 5.81 TB/s for k_gal_reg's own bytes and order
+// (profiles/r05b_kstream.txt).
+#ifndef GD_REG_Z16
+#define GD_REG_Z16 0  // bit 0: z loads, bit 1: zin stores (measured: +0.5 ... +2 %, off)
+#endif
+// the pair's 8 float4 (row 2p at c < 4, row 2p + 1 at 4 + c); r0 = row 2p + 4 j
+__device__ __forceinline__ void z16_load(f4v (&Z)[8], const float* r0, int L) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        Z[c] = ld4v(r0 + 64 * c);
+        Z[4 + c] = ld4v(r0 + L + 64 * c);
+    }
+}
+// Z -> X[r] = (x_2p[j + 16 r], x_2p+1[j + 16 r]) through xs (the line's exchange area); MAP(a, b) is applied to
+// each value first (e.g. max(y, 0) / alpha)
+template <typename F>
+__device__ __forceinline__ void z16_unpack(float2 (&X)[16], const f4v (&Z)[8], float2* xs, int j, F&& map) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const f4v a = Z[c], b = Z[4 + c];
+        *reinterpret_cast<f4v*>(xs + 4 * j + 64 * c) = f4v{map(a[0]), map(b[0]), map(a[1]), map(b[1])};
+        *reinterpret_cast<f4v*>(xs + 4 * j + 64 * c + 2) = f4v{map(a[2]), map(b[2]), map(a[3]), map(b[3])};
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) X[r] = xs[j + 16 * r];
+    wave_lds_sync();  // the reads complete before the line's FFT rewrites the area
+}
+// V[r] = (row 2p, row 2p + 1) at columns j + 16 r -> 16-byte non-temporal stores of both rows; o = row 2p
+__device__ __forceinline__ void z16_store(float* o, const float2 (&V)[16], float2* xs, int j, int L) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xs[j + 16 * r] = V[r];
+    wave_lds_sync();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const f4v a = *reinterpret_cast<const f4v*>(xs + 4 * j + 64 * c);
+        const f4v b = *reinterpret_cast<const f4v*>(xs + 4 * j + 64 * c + 2);
+        st4v(o + 4 * j + 64 * c, f4v{a[0], a[2], b[0], b[2]});
+        st4v(o + L + 4 * j + 64 * c, f4v{a[1], a[3], b[1], b[3]});
+    }
+    wave_lds_sync();
 }
 
 // Poisson pass A's bin (the X update and u1's dual, models/Unrolled_ADMM.py:209, :212, on spectra).  The
@@ -143,14 +202,14 @@ struct SGroup {
 template <int L, bool POIS = false>
 __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb, int kx, int q, int j, bool first,
                                             bool last) {
-    G.h = POIS ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_hh + gb + soff_h(kx, q, j));  // Poisson: |H|^2 from H
+    G.h = POIS ? f4v{0.f, 0.f, 0.f, 0.f} : ld4s(a.s_hh + gb + soff_h(kx, q, j));  // Poisson: |H|^2 from H
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const size_t off = gb + soff_c(kx, 2 * q + h, j);
         // Gaussian G (first: W~1 needs it; not on the last); Poisson: the OTF H (the G slot)
-        G.g[h] = (!POIS && last && !first) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_g + off);
-        G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4v(a.s_u1 + off);
-        G.w[h] = ld4v(a.s_w + off);
+        G.g[h] = (!POIS && last && !first) ? f4v{0.f, 0.f, 0.f, 0.f} : ld4s(a.s_g + off);
+        G.u[h] = first ? f4v{0.f, 0.f, 0.f, 0.f} : ld4s(a.s_u1 + off);
+        G.w[h] = ld4s(a.s_w + off);
     }
 }
 template <int L, int NC, bool POIS = false, int D = GD_REG_DEPTH>
@@ -251,17 +310,32 @@ struct RegGeo {
     static_assert(PK >= F2 && PXB >= 1 && RB0 + PXB <= RB1, "parking area above the exchange areas");
 };
 
-// Phase-locking: one galaxy per CU at a time, the same phase durations on every CU, so without an
-// offset all CUs load state together (HBM saturated) and then transform together (HBM idle).  Odd
-// workgroups of the first round start GD_REG_STAGGER microseconds late; CUs then keep the offset
-// from galaxy to galaxy.
+// Phase-locking: one galaxy per CU at a time, the same phase durations on every CU, so every launch starts with
+// all 256 CUs loading z together (HBM saturated), then transforming together (HBM idle), and the lock decays only
+// over ~6 of the launch's 16 rounds (round-5 phase trace of 4096 x 256^2: the first round takes 139 us per galaxy
+// against ~100 later; profiles/r05_reg_lockstep.txt).  The first round's workgroups g < 256 therefore start in
+// GD_STAGGER_N groups spread over the given microseconds (group g mod N waits (g mod N) / N of it; the z / y loads
+// are issued before the wait, so their latency runs during it).  A/B at 4096 x 256^2 (profiles/r05_stagger_ab.txt):
+// k_gal_reg MID 1.646-1.650 -> 1.624-1.631 ms, FIRST 1.41 -> 1.39 ms, LAST unchanged; k_gal_reg_init 1.365 -> 1.320-
+// 1.337 ms; k_rl_reg unchanged (not applied).
 #ifndef GD_REG_STAGGER
-#define GD_REG_STAGGER 0
+#define GD_REG_STAGGER 60  // k_gal_reg: total spread of the first round's start times, microseconds
 #endif
+#ifndef GD_INIT_STAGGER
+#define GD_INIT_STAGGER 60  // k_gal_reg_init
+#endif
+#ifndef GD_RL_STAGGER
+#define GD_RL_STAGGER 0  // k_rl_reg
+#endif
+#ifndef GD_STAGGER_N
+#define GD_STAGGER_N 4  // groups of the first round (group k starts k / N of the spread late)
+#endif
+template <int US>
 __device__ __forceinline__ void stagger_start(int g) {
-    if (GD_REG_STAGGER > 0 && g < 256 && (g & 1)) {
+    if (US > 0 && g < 256 && (g % GD_STAGGER_N) != 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)GD_REG_STAGGER * 100) __builtin_amdgcn_s_sleep(32);
+        const unsigned long long d = (unsigned long long)US * 100 * (g % GD_STAGGER_N) / GD_STAGGER_N;
+        while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(32);
     }
 }
 
@@ -291,11 +365,19 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     const bool first = __builtin_amdgcn_readfirstlane(a.first) != 0, last = __builtin_amdgcn_readfirstlane(a.last) != 0;
     const float r2n = (POIS || last) ? 0.f : a.rho2n(g);
     const float al = POIS ? a.alpha(g) : 1.f;
-    stagger_start(g);
     GD_TRACE(0);
 
     // R
     float2 X[RG::PPL][F2];
+#if GD_REG_Z16 & 1
+    f4v Z4[RG::PPL][8];
+    {
+        const float* z = a.a0 + (size_t)g * L * L;
+#pragma unroll
+        for (int q = 0; q < RG::PPL; ++q)
+            z16_load(Z4[q], z + (size_t)(2 * (opaque(line) + LINES * q)) * L + 4 * opaque(j), L);
+    }
+#else
     {
         const float* z = a.a0 + (size_t)g * L * L;
 #pragma unroll
@@ -306,10 +388,15 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
         }
     }
+#endif
+    stagger_start<GD_REG_STAGGER>(g);  // (z's loads are in flight meanwhile)
     __syncthreads();  // twiddles
     GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < RG::PPL; ++q) {
+#if GD_REG_Z16 & 1
+        z16_unpack(X[q], Z4[q], my, opaque(j), [](float v) { return v; });
+#endif
         reg_fft<L, false>(X[q], opaque(j), my, tw);
         pin(X[q]);
         __builtin_amdgcn_sched_barrier(0);
@@ -484,18 +571,22 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
             reg_fft<L, true>(V[w], opaque(j), my, tw);
-            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
             if constexpr (POIS) {
                 if (last) {  // x * alpha for Poisson (:215)
 #pragma unroll
                     for (int r = 0; r < F2; ++r) V[w][r] = make_float2(V[w][r].x * al, V[w][r].y * al);
                 }
             }
+#if GD_REG_Z16 & 2
+            z16_store(out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L, V[w], my, opaque(j), L);
+#else
+            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) {
                 st_s(o + F1 * r, V[w][r].x);
                 st_s(o + L + F1 * r, V[w][r].y);
             }
+#endif
         }
     });
     drain_vm();  // the LDS-DMA warm loads land before the workgroup (and its LDS) is gone
@@ -646,6 +737,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) * ial, fmaxf(r0[L + F1 * r], 0.f) * ial);
         }
     }
+    stagger_start<GD_INIT_STAGGER>(g);
     __syncthreads();  // twiddles
     GD_TRACE(1);
 #pragma unroll

@@ -147,6 +147,107 @@ __global__ __launch_bounds__(512) void k_mix(const float* z, float* zin, const f
     }
 }
 
+// ---- (3) k_gal_reg's own access pattern with no compute: 512 threads = 32 lines of 16 lanes, 4 lines per wave.
+//   z: pair p = line + 32 q (q < 4), lane j loads rows 2p, 2p + 1 at j + 16 r (4-byte loads, 64 B per line and
+//      instruction); zin stored the same way (phase I), after the state;
+//   state: slice A (columns line + 32 u, u < 2) then slice B (64 + ...), per column 4 groups q of 4 bins x 16 lanes,
+//      one 16-byte |H|^2 load and two each of G, U1, W~ per group, D groups in flight (fused_update4x's order);
+//   LAYOUT 0: the engine's [kx][256] columns (soff_c / soff_h); 1: columns interleaved in quads of 4 (kx >> 2):
+//      the 4 columns a wave holds (lines 4w .. 4w + 3) are adjacent per 256-byte group, so one wave instruction
+//      reads 1 KiB contiguous.
+template <int LAYOUT>
+__device__ __forceinline__ int qoff_c(int kx, int m, int j) {  // float2 units, bins j + 16 (2m + e)
+    if constexpr (LAYOUT == 0) return kx * 256 + 32 * m + 2 * j;
+    else return (kx >> 2) * 1024 + 128 * m + 32 * (kx & 3) + 2 * j;
+}
+template <int LAYOUT>
+__device__ __forceinline__ int qoff_h(int kx, int q, int j) {  // floats, bins j + 16 (4q + e)
+    if constexpr (LAYOUT == 0) return kx * 256 + 64 * q + 4 * j;
+    else return (kx >> 2) * 1024 + 256 * q + 64 * (kx & 3) + 4 * j;
+}
+template <int LAYOUT, int D, bool Z16>
+__global__ __launch_bounds__(512) void k_regpat(const float* z, float* zin, const float* hh, const float2* G, float2* Uu,
+                                                float2* W, int N) {
+    __shared__ float pad[36000];
+    const int g = blockIdx.x, tid = threadIdx.x, line = tid >> 4, j = tid & 15;
+    if (tid == 0) pad[g & 1023] = 0.f;
+    const float* zg = z + g * IMG;
+    float* og = zin + g * IMG;
+    float2 X[4][16];
+    if constexpr (Z16) {  // the same bytes per thread as 16-byte loads (1 KiB per wave instruction)
+        const f4v* z4 = reinterpret_cast<const f4v*>(zg);
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const f4v v = z4[tid + 512 * u];
+            X[u >> 3][2 * (u & 7)] = make_float2(v[0], v[1]);
+            X[u >> 3][2 * (u & 7) + 1] = make_float2(v[2], v[3]);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float* r0 = zg + (size_t)(2 * (line + 32 * q)) * 256 + j;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) X[q][r] = make_float2(r0[16 * r], r0[256 + 16 * r]);
+        }
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc += X[q][r].x - X[q][r].y;
+    pad[tid] = acc;
+    const size_t gb = (size_t)g * SPEC;
+    const float* hg = hh + gb;
+    const float2 *Gg = G + gb;
+    float2 *Ug = Uu + gb, *Wg = W + gb;
+    for (int slice = 0; slice < 2; ++slice) {
+        __syncthreads();
+        constexpr int NG = 8;  // 2 columns x 4 groups
+        f4v h[NG], g0[NG], g1[NG], u0[NG], u1[NG], w0[NG], w1[NG];
+        auto load = [&](int t) {
+            const int kx = 64 * slice + line + 32 * (t >> 2), q = t & 3;
+            h[t] = *reinterpret_cast<const f4v*>(hg + qoff_h<LAYOUT>(kx, q, j));
+            g0[t] = *reinterpret_cast<const f4v*>(Gg + qoff_c<LAYOUT>(kx, 2 * q, j));
+            g1[t] = *reinterpret_cast<const f4v*>(Gg + qoff_c<LAYOUT>(kx, 2 * q + 1, j));
+            u0[t] = *reinterpret_cast<const f4v*>(Ug + qoff_c<LAYOUT>(kx, 2 * q, j));
+            u1[t] = *reinterpret_cast<const f4v*>(Ug + qoff_c<LAYOUT>(kx, 2 * q + 1, j));
+            w0[t] = *reinterpret_cast<const f4v*>(Wg + qoff_c<LAYOUT>(kx, 2 * q, j));
+            w1[t] = *reinterpret_cast<const f4v*>(Wg + qoff_c<LAYOUT>(kx, 2 * q + 1, j));
+        };
+#pragma unroll
+        for (int t = 0; t < D; ++t) load(t);
+#pragma unroll
+        for (int t = 0; t < NG; ++t) {
+            const int kx = 64 * slice + line + 32 * (t >> 2), q = t & 3;
+            st<true>(reinterpret_cast<f4v*>(Ug + qoff_c<LAYOUT>(kx, 2 * q, j)), u0[t] + g0[t] * h[t].x);
+            st<true>(reinterpret_cast<f4v*>(Ug + qoff_c<LAYOUT>(kx, 2 * q + 1, j)), u1[t] + g1[t] * h[t].y);
+            st<true>(reinterpret_cast<f4v*>(Wg + qoff_c<LAYOUT>(kx, 2 * q, j)), w0[t] - g0[t]);
+            st<true>(reinterpret_cast<f4v*>(Wg + qoff_c<LAYOUT>(kx, 2 * q + 1, j)), w1[t] - g1[t]);
+            if (t + D < NG) load(t + D);
+        }
+    }
+    __syncthreads();
+    const float s = pad[(tid + 1) & 511];
+    if constexpr (Z16) {
+        f4v* o4 = reinterpret_cast<f4v*>(og);
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const float2 a = X[u >> 3][2 * (u & 7)], b = X[u >> 3][2 * (u & 7) + 1];
+            st<true>(o4 + tid + 512 * u, f4v{a.x * s, a.y * s, b.x * s, b.y * s});
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float* o = og + (size_t)(2 * (line + 32 * q)) * 256 + j;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                __builtin_nontemporal_store(X[q][r].x * s, o + 16 * r);
+                __builtin_nontemporal_store(X[q][r].y * s, o + 256 + 16 * r);
+            }
+        }
+    }
+}
+
 // ---- timing: median of 5 timed blocks of reps launches each
 template <typename F>
 float time_ms(F&& f, int reps) {
@@ -240,6 +341,14 @@ int main(int argc, char** argv) {
         MIX(false, true, 1, true) MIX(false, true, 2, true) MIX(false, true, 4, true)
         MIX(true, false, 2, true) MIX(true, true, 1, true) MIX(true, true, 2, true) MIX(true, true, 4, true)
         MIX(false, true, 2, false) MIX(true, true, 2, false)
+#define REGPAT(LAY, D, Z16)                                                                                          \
+    {                                                                                                                \
+        const float ms = time_ms([&] { hipLaunchKernelGGL((k_regpat<LAY, D, Z16>), dim3(N), dim3(512), 0, 0, z, zin, hh, G, Uu, W, N); }, reps); \
+        CK(hipGetLastError());                                                                                       \
+        printf("k_gal_reg pattern layout=%d D=%d z16=%d N=%d  %.3f ms  %.3f TB/s (%.3f GB)\n", LAY, D, Z16, N, ms, gb / ms, gb); \
+    }
+        REGPAT(0, 2, false) REGPAT(0, 4, false) REGPAT(1, 2, false) REGPAT(1, 4, false) REGPAT(0, 2, true) REGPAT(1, 2, true)
+        REGPAT(1, 8, true)
     }
     return 0;
 }
