@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -2351,17 +2352,32 @@ int g_subnet_fused_max = 256;
 int g_sri_map = 0;  // k_subnet_rhos_init's block -> (role, galaxy) map (tools/kbench_small)
 int g_fused_init = 1;  // Gaussian init (256^2: k_psf_rows<STATE> + k_gal_reg_init) and the other one-launch inits: 1 on; 0 = chunked
 
+// Under stream capture a pipelined operation takes its fork / join events from a ring of kCapSets sets, so no event
+// is recorded twice inside one captured forward (GD_CAPTURE_PIPELINE, below).
+constexpr int kCapSets = 64;
 struct PipeRes {
     bool ok = false;
     hipStream_t st[kMaxPipe];
     hipEvent_t fork;
     hipEvent_t join[kMaxPipe];
+    hipEvent_t cfork[kCapSets];
+    hipEvent_t cjoin[kCapSets][kMaxPipe];
+    int cpos = 0;
     // held from the fork record to the last join wait of one pipelined call: the fork / join events and
     // the internal streams are per device, so concurrent callers (host threads) enqueue one at a time
     std::mutex mu;
 };
 PipeRes g_pipe[64];
 std::mutex g_pipe_mu;
+
+thread_local int g_capture_pipe_override = -1;  // gd_set_capture_pipeline (per host thread)
+inline int capture_pipeline_mode() {
+    static const int mode = [] {
+        const char* e = std::getenv("GD_CAPTURE_PIPELINE");
+        return e ? std::atoi(e) : 2;
+    }();
+    return g_capture_pipe_override >= 0 ? g_capture_pipe_override : mode;
+}
 
 inline PipeRes* pipe_res() {
     int dev = 0;
@@ -2374,6 +2390,11 @@ inline PipeRes* pipe_res() {
             if (hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming) != hipSuccess) return nullptr;
         }
         if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+        for (int c = 0; c < kCapSets; ++c) {
+            if (hipEventCreateWithFlags(&r.cfork[c], hipEventDisableTiming) != hipSuccess) return nullptr;
+            for (int i = 0; i < kMaxPipe; ++i)
+                if (hipEventCreateWithFlags(&r.cjoin[c][i], hipEventDisableTiming) != hipSuccess) return nullptr;
+        }
         r.ok = true;
     }
     return &r;
@@ -2420,19 +2441,39 @@ int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
     if (G >= a.N) return f(a, st);
     int S = g_pipe_streams < kMaxPipe ? g_pipe_streams : kMaxPipe;
     if (S > a.N / G) S = a.N / G;  // regions must fit the caller's workspace
-    // Under stream capture the chunks go in sequence on the caller's stream: instantiating a graph that
-    // holds this fork / join (the same events recorded once per pipelined operation) crashed the ROCm 7
-    // runtime inside hipStreamEndCapture at 4096 x 160^2 (profiles/r04dbg_160_graph_crash.txt)
+    // Under stream capture (GD_CAPTURE_PIPELINE, or gd_set_capture_pipeline per host thread): 0 = the chunks in
+    // sequence on the caller's stream; 1 = pipelined with the shared fork / join events; 2 = pipelined, each
+    // operation's fork / join on its own event set from the ring (default).  Round 5 (profiles/r05_capture_*):
+    // the round-4 crash inside hipStreamEndCapture (4096 x 160^2, profiles/r04dbg_160_graph_crash.txt) is not the
+    // event re-use - mode 2 crashes the same way - but a fork from a stream that itself joined the capture through
+    // an event (ADMMState.init_concurrent's side stream) onto these internal streams, inside torch's capture:
+    // forked from the capturing stream itself, mode 2 captures, instantiates and replays bit-identically.  The
+    // same fork / join in plain HIP (tools/capture_probe.hip: shared or fresh events, nested, streams created
+    // during the capture, temporary events destroyed) does not crash.  So the engine runs a side-stream init with
+    // mode 0 under capture (gdeconv/engine.py) and everything else with mode 2.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (S > 1 && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) S = 1;
+    const bool capturing = S > 1 && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+    const int cmode = capture_pipeline_mode();
+    if (capturing && cmode == 0) S = 1;
     PipeRes* r = S > 1 ? pipe_res() : nullptr;
     if (!r) S = 1;
     std::unique_lock<std::mutex> lk;
     if (S > 1) lk = std::unique_lock<std::mutex>(r->mu);
+    hipEvent_t fork = nullptr;
+    hipEvent_t* join = nullptr;
     if (S > 1) {
-        if (hipEventRecord(r->fork, st) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
+        if (capturing && cmode == 2) {
+            const int c = r->cpos;
+            r->cpos = (c + 1) % kCapSets;
+            fork = r->cfork[c];
+            join = r->cjoin[c];
+        } else {
+            fork = r->fork;
+            join = r->join;
+        }
+        if (hipEventRecord(fork, st) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
         for (int i = 0; i < S; ++i)
-            if (hipStreamWaitEvent(r->st[i], r->fork, 0) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
+            if (hipStreamWaitEvent(r->st[i], fork, 0) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
     }
     int rc = GD_OK;
     for (int g0 = 0, c = 0; g0 < a.N && rc == GD_OK; g0 += G, ++c) {
@@ -2443,7 +2484,7 @@ int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
     }
     if (S > 1) {
         for (int i = 0; i < S; ++i) {
-            if (hipEventRecord(r->join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(st, r->join[i], 0) != hipSuccess)
+            if (hipEventRecord(join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(st, join[i], 0) != hipSuccess)
                 return fail(GD_ERR_HIP, "pipeline join");
         }
     }
@@ -3169,6 +3210,12 @@ int gd_profile_reset(void) {
 size_t gd_set_chunk_bytes(size_t bytes) {
     const size_t old = g_chunk_bytes;
     g_chunk_bytes = bytes;
+    return old;
+}
+
+int gd_set_capture_pipeline(int mode) {
+    const int old = g_capture_pipe_override;
+    g_capture_pipe_override = (mode >= 0 && mode <= 2) ? mode : -1;
     return old;
 }
 

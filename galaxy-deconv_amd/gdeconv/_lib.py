@@ -53,6 +53,7 @@ SIGNATURES = {
     "gd_gx_xupdate_backward": (_I, [_P, _P, _P, _LL, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "gd_set_chunk_bytes": (_SZ, [_SZ]),
     "gd_set_pipeline_streams": (_I, [_I]),
+    "gd_set_capture_pipeline": (_I, [_I]),
     "gd_set_fused_iteration": (_I, [_I]),
     "gd_set_fused_rl": (_I, [_I]),
     "gd_set_subnet_fused_max": (_I, [_I]),

@@ -581,7 +581,8 @@ class ADMMState:
 
     _reads_rho = {}     # (H, W, llh) -> forced gd_admm_init_reads_rho (overrides for tests; empty by default)
     _state_bytes = {}   # (N, H, W, llh) -> gd_admm_state_bytes (pure in its arguments)
-    _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (created once)
+    _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (LRU, bounded)
+    _SIDE_STREAMS_MAX = 16
 
     @property
     def otf(self):
@@ -646,14 +647,27 @@ class ADMMState:
             raise ValueError("this init takes the first V step: it needs the rhos (use init(rho2_first))")
         main = torch.cuda.current_stream(self.dev)
         # one side stream per (device, caller's stream): two host threads forwarding on their own streams
-        # do not serialise their inits on a shared side stream (nor join each other's)
+        # do not serialise their inits on a shared side stream (nor join each other's); a bounded cache, so
+        # the streams of callers that come and go are not kept forever
         key = (self._dev_index, main.cuda_stream)
-        side = ADMMState._side_streams.get(key)
+        side = ADMMState._side_streams.pop(key, None)
         if side is None:
-            side = ADMMState._side_streams[key] = torch.cuda.Stream(device=self.dev)
+            side = torch.cuda.Stream(device=self.dev)
+        ADMMState._side_streams[key] = side          # most recently used last
+        while len(ADMMState._side_streams) > ADMMState._SIDE_STREAMS_MAX:
+            ADMMState._side_streams.pop(next(iter(ADMMState._side_streams)))
         side.wait_stream(main)
-        with torch.cuda.stream(side):
-            self.init(None)
+        # under stream capture a chunked init on the side stream runs its chunks in sequence: a fork from a
+        # stream that joined the capture through an event onto the library's pipeline streams crashed the ROCm 7
+        # runtime inside hipStreamEndCapture (gd_set_capture_pipeline)
+        capturing = torch.cuda.is_current_stream_capturing()
+        old = self.lib.gd_set_capture_pipeline(0) if capturing else None
+        try:
+            with torch.cuda.stream(side):
+                self.init(None)
+        finally:
+            if capturing:
+                self.lib.gd_set_capture_pipeline(old)
         self._side = side
 
     def join(self):

@@ -218,6 +218,13 @@ int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride,
 size_t gd_set_chunk_bytes(size_t bytes);
 int gd_set_pipeline_streams(int streams);
 
+/* Chunk pipelining under stream capture, for the CALLING HOST THREAD only: mode 2 (the default) forks a captured
+ * operation's chunks onto the internal streams with an event set of its own, 0 runs them in sequence on the
+ * capturing stream (use it when enqueuing from a stream that joined the capture through an event: such a nested
+ * fork crashed the ROCm 7 runtime inside hipStreamEndCapture), 1 reuses one event set; -1 restores the default
+ * (the GD_CAPTURE_PIPELINE environment variable, else 2).  Returns the previous override (-1: none). */
+int gd_set_capture_pipeline(int mode);
+
 /* Fused iterations: at the sizes that have them (see "sizes" above; Poisson at 256^2 and square L <= 112)
  * gd_admm_iter runs one workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic).
  * on != 0 (default 1) selects them; 0 selects the chained path (row pass / column pass / row pass through

@@ -52,17 +52,20 @@ def test_graphed_forward_engine_bit_identical(dev, L, N, llh):
     assert torch.equal(g(obs2, psf2, alpha2), eager2)
 
 
+@pytest.mark.parametrize("mode", [2, 0])
 @pytest.mark.parametrize("H,W", [(100, 100), (90, 72)])
-def test_graphed_forward_chunked_pipeline(dev, H, W):
+def test_graphed_forward_chunked_pipeline(dev, H, W, mode):
     """A forward whose runtime-planned operations run in several Infinity-Cache chunks (chunk bytes
     forced down to two galaxies; the 4096 x 160^2 bench line did the same at 96 MiB before 160^2 was fused)
-    captures and replays bit-identically; the chunks go in sequence under capture."""
+    captures and replays bit-identically, with the chunks pipelined over the internal streams under capture
+    (gd_set_capture_pipeline 2, the default: an event set per operation) or in sequence (0)."""
     from gdeconv import _lib
     from gdeconv.graphs import GraphedForward
     from gdeconv.synth import make_batch
     lib = _lib.load()
     tgal = 2 * (W // 2 + 1) * H * 8
     old = lib.gd_set_chunk_bytes(2 * tgal)
+    old_mode = lib.gd_set_capture_pipeline(mode)
     try:
         m = _model(8, "Gaussian", dev, identity=True)
         obs, psf, alpha, _ = make_batch(7, H, W, seed=11, device=dev)
@@ -72,6 +75,34 @@ def test_graphed_forward_chunked_pipeline(dev, H, W):
         assert torch.equal(g(obs, psf, alpha), eager)
     finally:
         lib.gd_set_chunk_bytes(old)
+        lib.gd_set_capture_pipeline(old_mode)
+
+
+def test_graphed_forward_side_stream_chunked_init(dev):
+    """The round-4 capture crash's shape, scaled down: a batch large enough for the init to run on a side stream
+    beside the SubNet (models.CONCURRENT_INIT_PIXELS), the chunked runtime-planned Gaussian init (fused init off)
+    in 6 chunks, captured and replayed bit-identically.  The side-stream init runs its chunks in sequence under
+    capture (engine.ADMMState.init_concurrent), the iterations pipeline theirs."""
+    from gdeconv import _lib
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.models import CONCURRENT_INIT_PIXELS
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    H = W = 160
+    N = -(-CONCURRENT_INIT_PIXELS // (H * W)) + 2
+    tgal = 2 * (W // 2 + 1) * H * 8
+    old = lib.gd_set_chunk_bytes((N // 6 + 1) * tgal)
+    old_fi = lib.gd_set_fused_init(0)
+    try:
+        m = _model(8, "Gaussian", dev, identity=True)
+        obs, psf, alpha, _ = make_batch(N, H, W, seed=13, device=dev)
+        with torch.no_grad():
+            eager = m(obs, psf, alpha)
+        g = GraphedForward(m, obs, psf, alpha, clone=True)
+        assert torch.equal(g(obs, psf, alpha), eager)
+    finally:
+        lib.gd_set_chunk_bytes(old)
+        lib.gd_set_fused_init(old_fi)
 
 
 def test_graphed_forward_full_model(dev):
