@@ -89,6 +89,7 @@ struct Args {
     float2* s_x;           // Poisson two-pass at 256^2: X (pass A -> pass B), state layout as s_u1
     int gH, gW;            // image rows / columns (the runtime-size path, gd_generic.hpp)
     int pw;                // PSF columns when the PSF is h x pw, not square (0 = h; the runtime-size path)
+    int rev;               // k_gal_reg: workgroup b runs galaxy N - 1 - b (the previous launch's last galaxies first)
 };
 
 enum RowFwdMode { RF_ITER, RF_PSF_Y, RF_PSF_YP, RF_PSF_RAW, RF_PSF, RF_ONE, RF_TWO, RF_YA, RF_PSF_YAR,
@@ -2495,6 +2496,9 @@ int for_chunks(const Args& a, int L, hipStream_t st, F&& f) {
     return for_chunks_hw(a, L, L, st, std::forward<F>(f));
 }
 
+#ifndef GD_REG_REV
+#define GD_REG_REV 1
+#endif
 #ifndef GD_POIS_SMALL
 #define GD_POIS_SMALL 1  // 1: Poisson iterations at L <= 112 in one launch (k_pois_small); 0: the three-kernel chain
 #endif
@@ -3013,6 +3017,10 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     a.llh = llh;
     a.last = last;
     a.first = iter == 0;
+    // k_gal_reg's galaxy order alternates from launch to launch (the init runs forward; Poisson's pass B forward,
+    // pass A reversed), so a launch starts on the galaxies the previous one finished with - their state, z and
+    // zin are the last ~256 MB of traffic, still in the Infinity Cache (GD_REG_REV)
+    a.rev = GD_REG_REV ? (llh == GD_LLH_POISSON ? 1 : (iter % 2 == 0)) : 0;
     ProfScope ps("op_admm_iter<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN) {
         a.a0 = z;

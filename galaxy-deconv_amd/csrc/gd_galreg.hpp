@@ -357,7 +357,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     __shared__ float nyqo[L];       // x(., L/2)
     __shared__ float4 pf_sink[64];  // warm_next's LDS-DMA target (never read)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
-    const int g = blockIdx.x;
+    const int b = blockIdx.x, g = a.rev ? a.N - 1 - b : b;
     const bool l0 = (line == 0);
     float2* my = S + line * RG::XCH;
     fill_twiddles<L>(tw, tid, T);
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         }
     }
 #endif
-    stagger_start<GD_REG_STAGGER>(g);  // (z's loads are in flight meanwhile)
+    stagger_start<GD_REG_STAGGER>(b);  // (z's loads are in flight meanwhile)
     __syncthreads();  // twiddles
     GD_TRACE(1);
 #pragma unroll

@@ -190,8 +190,10 @@ int main(int argc, char** argv) {
         printf("k_stream<512>  (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m5, gb[0] / m5);
         printf("k_stream<1024> (MID bytes) N=%d  %.3f ms  %.2f TB/s\n", N, m10, gb[0] / m10);
     }
+    // KB_REV=1: consecutive launches alternate the galaxy order (Args::rev), as gd_admm_iter does
+    const bool alt = getenv("KB_REV") && atoi(getenv("KB_REV"));
     for (int fl = 0; fl < 3; ++fl) {
-        const float ms = time_ms([&] { launch_v(1, fl, t.a); }, reps);
+        const float ms = time_ms([&] { if (alt) t.a.rev ^= 1; launch_v(1, fl, t.a); }, reps);
         CK(hipGetLastError());
         printf("k_gal_reg<256,%-5s> N=%d  %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", fln[fl], N, ms, gb[fl] / ms, gb[fl]);
     }
