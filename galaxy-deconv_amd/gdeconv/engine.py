@@ -390,7 +390,8 @@ class GaussXState:
         nbytes = int(self.lib.gd_gx_state_bytes(N1, self.H, self.W))
         if nbytes == 0:
             raise ValueError(f"UnrolledADMMGaussian: unsupported image size {self.H}x{self.W} "
-                             "(even sides 2 .. 512: the 2x padded grid must fit the engine)")
+                             "(even sides 2 .. 818: the 2x padded grid must fit the engine; the reference itself "
+                             "fails on odd sides, its crop_half(pad_double(.)) returning H - 1 rows)")
         with _on(self.dev):
             self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
             self.state = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)

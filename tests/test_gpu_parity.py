@@ -663,16 +663,16 @@ def _gauss_state_parts(st):
     return hh, c[:spec].reshape(N, K, L, 2), c[2 * spec:3 * spec].reshape(N, K, L, 2)
 
 
+@pytest.mark.parametrize("N", [37, 300])
 @pytest.mark.parametrize("variant", [1])
 @pytest.mark.parametrize("h", [48, 32, 64])
-def test_fused_init_matches_chunked_chain(dev, h, variant):
+def test_fused_init_matches_chunked_chain(dev, h, variant, N):
     """k_psf_rows<TO_STATE> + k_gal_reg_init (one launch: y -> |H|^2, G, x0 = clamp -> zin, F(x0) -> W~) against
     the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain: the whole Gaussian state and
-    zin, per-galaxy PSFs / alpha / rho2, ragged batch (37)."""
+    zin, per-galaxy PSFs / alpha / rho2, ragged batches (37 and 300, more galaxies than CUs)."""
     from gdeconv import _lib, engine
     from gdeconv.synth import make_batch
     lib = _lib.load()
-    N = 37
     obs, psf, alpha, _ = make_batch(N, 256, h=h, seed=90 + h, device=dev)
     r2 = (0.5 + torch.rand(N, generator=torch.Generator().manual_seed(h))).to(dev)
     outs = []
