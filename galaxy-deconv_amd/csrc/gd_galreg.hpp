@@ -212,9 +212,25 @@ __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb,
         G.w[h] = ld4s(a.s_w + off);
     }
 }
+// GD_REG_SPF: the first D groups of a slice's state are loaded BEFORE the slice's forward column FFTs
+// (fused_prefetch4x), so their latency runs under the transforms instead of opening the update
+#ifndef GD_REG_SPF
+#define GD_REG_SPF 1
+#endif
 template <int L, int NC, bool POIS = false, int D = GD_REG_DEPTH>
+__device__ __forceinline__ void fused_prefetch4x(const Args& a, SGroup (&P)[D], int g, int kx0, int kstep, int j, bool first,
+                                                 bool last) {
+    j = opaque(j);
+    kx0 = opaque(kx0);
+    const size_t gb = (size_t)g * (L / 2 + 1) * L;
+#pragma unroll
+    for (int t = 0; t < D && t < 4 * NC; ++t) sgroup_load<L, POIS>(a, P[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int L, int NC, bool POIS = false, int D = GD_REG_DEPTH, bool PRE = false>
 __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16], int g, int kx0, int kstep, int j,
-                                               float r1, float r2, float r2n, bool first, bool last) {
+                                               float r1, float r2, float r2n, bool first, bool last,
+                                               const SGroup (*pre)[D] = nullptr) {
     constexpr float inv_n = float(1.0 / double(L * L));
     constexpr int NG = 4 * NC;
     j = opaque(j);
@@ -223,7 +239,10 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
     const size_t gb = (size_t)g * (L / 2 + 1) * L;
     SGroup G[NG];
 #pragma unroll
-    for (int t = 0; t < D && t < NG; ++t) sgroup_load<L, POIS>(a, G[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
+    for (int t = 0; t < D && t < NG; ++t) {
+        if constexpr (PRE) G[t] = (*pre)[t];
+        else sgroup_load<L, POIS>(a, G[t], gb, kx0 + kstep * (t / 4), t % 4, j, first, last);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < NG; ++t) {
@@ -438,6 +457,10 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tid] = X[q][r];
     __builtin_amdgcn_sched_barrier(0);
     GD_TRACE(3);
+    constexpr int DPT = POIS ? GD_POIS_DEPTH : GD_REG_DEPTH;
+    constexpr bool SPF = GD_REG_SPF && !POIS;
+    SGroup preA[DPT];
+    if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preA, g, line, LINES, j, first, last);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, false>(CA[u], opaque(j), my, tw);
@@ -460,7 +483,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     if (__builtin_amdgcn_readfirstlane(tid >> 6) < L / 64) {
         nyqc[tid] = gauss_bin4<L, POIS>(a, g, tid, nyqc[tid], r1, r2, r2n, first, last);
     }
-    fused_update4x<L, RG::CPL, POIS, POIS ? GD_POIS_DEPTH : GD_REG_DEPTH>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last);
+    fused_update4x<L, RG::CPL, POIS, DPT, SPF>(a, CA, g, line, LINES, j, r1, r2, r2n, first, last, &preA);
     lds_barrier();  // Nyquist results
     GD_TRACE(4);
 #pragma unroll
@@ -510,14 +533,15 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     for (int s = 0; s < F2; ++s) park[s * T + tid] = CA[RG::CPL - 1][s];
     __builtin_amdgcn_sched_barrier(0);
     GD_TRACE(6);
+    SGroup preB[DPT];
+    if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preB, g, KS + line, LINES, j, first, last);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, false>(CB[u], opaque(j), my, tw);
         if (GD_REG_PINF) pin(CB[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
-    fused_update4x<L, RG::CPL, POIS, POIS ? GD_POIS_DEPTH : GD_REG_DEPTH>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first,
-                                                                      last);
+    fused_update4x<L, RG::CPL, POIS, DPT, SPF>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last, &preB);
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CB[u], opaque(j), my, tw);
