@@ -595,6 +595,10 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
             reg_fft<L, true>(V[w], opaque(j), my, tw);
+#if !(GD_REG_Z16 & 2)
+            // (the row pointer ahead of Poisson's scaling: formed after it, pass A spilled 4 VGPRs)
+            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
+#endif
             if constexpr (POIS) {
                 if (last) {  // x * alpha for Poisson (:215)
 #pragma unroll
@@ -604,7 +608,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #if GD_REG_Z16 & 2
             z16_store(out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L, V[w], my, opaque(j), L);
 #else
-            float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) {
                 st_s(o + F1 * r, V[w][r].x);
