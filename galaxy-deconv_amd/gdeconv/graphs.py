@@ -5,9 +5,12 @@ a few hundred galaxies) one ``Unrolled_ADMM`` forward is a chain of ~60 short la
 OTF, init_l2, 8 x (denoiser, spectral iteration) - and the host, not the GPU, sets the pace.
 ``GraphedForward`` records the forward once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm)
 and replays it: the engine's C ABI enqueues on torch's current stream and allocates nothing of its
-own; under capture its Infinity-Cache chunks run in sequence on that stream (the eager path forks them
-onto internal streams with events - a fork / join the ROCm 7 runtime crashed on when instantiating the
-graph, ``profiles/r04dbg_160_graph_crash.txt``).
+own.  Under capture its Infinity-Cache chunks are still pipelined onto the engine's internal streams
+(a fork / join per operation, each with its own captured event set, ``gd_set_capture_pipeline``);
+only an init that ``ADMMState.init_concurrent`` runs on a side stream keeps its chunks serial there:
+a fork nested inside that side stream's own fork was what crashed the ROCm 7 runtime when the graph
+was instantiated (``profiles/r04dbg_160_graph_crash.txt``, root cause in
+``profiles/r05b_capture_probe.txt``).
 
     g = GraphedForward(model, obs, psf, alpha)     # shapes fixed at capture
     rec = g(obs2, psf2, alpha2)                    # copies inputs in, replays, returns the output
