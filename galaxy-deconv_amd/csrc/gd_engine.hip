@@ -2309,10 +2309,9 @@ struct Launcher {
         hipLaunchKernelGGL((k_gal_reg_init<L, true>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a);
         return check_launch("k_gal_reg_init<POIS>");
     }
-    template <bool COTF>
     static int rl_reg(const Args& a, int n_iters, hipStream_t st) {
         ProfScope ps(nm("k_rl_reg", 0), st);
-        hipLaunchKernelGGL((k_rl_reg<L, COTF>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a, n_iters);
+        hipLaunchKernelGGL((k_rl_reg<L>), dim3(a.N), dim3(RegGeo<L>::THREADS), 0, st, a, n_iters);
         return check_launch("k_rl_reg");
     }
     static int gal_reg_init(const Args& a, hipStream_t st) {
@@ -2346,8 +2345,7 @@ size_t g_chunk_bytes = size_t(96) << 20;  // workspace (spectra) bytes per chunk
 int g_pipe_streams = 2;                   // measured best at 256^2: 2 streams x 96 MiB (186 galaxies)
 constexpr int kMaxPipe = 8;
 int g_fused = 1;  // Gaussian iterations (and Poisson ones at 256^2 / L <= 112): 1 = the one-launch kernels; 0 = chained
-int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg with the OTF built in the kernel (PSF side <= 64),
-                       // 2 = k_rl_reg reading the stored OTF, 0 = chunked chain
+int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per galaxy), 0 = chunked chain
 // gd_subnet_rhos_psf: one fused launch per galaxy up to this batch (one round of workgroups on the 256 CUs:
 // 60.5 vs 75.5 us at 256 x 48^2), else the feature kernel + batched MLP (1024: 173 vs 212 us; 4096: 584 vs
 // 818 us fused - each fused workgroup re-reads the MLP weights, and 129 VGPRs allow one per CU)
@@ -2702,18 +2700,10 @@ struct Ops {
     }
     static int richardson_lucy(Args a0, int n_iters, hipStream_t st0) {
         if constexpr (has_fused<L>()) {
-            if (g_fused_rl == 1 && n_iters > 0 && a0.h <= 64) {
-                // the PSF's compact row spectra into the OTF buffer, then every galaxy's whole loop in one
-                // launch, each column's OTF transformed in the kernel (gd_rlreg.hpp, COTF)
-                Args a1 = a0;
-                a1.s_u1 = a0.otf;
-                GD_TRY(Lc::psf_rows_state(a1, st0));
-                return Lc::template rl_reg<true>(a1, n_iters, st0);
-            }
             if (g_fused_rl && n_iters > 0) {
                 // the OTF (chunked psf_to_otf), then every galaxy's whole loop in one launch
                 GD_TRY(for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) { return psf_to_otf(a, st); }));
-                return Lc::template rl_reg<false>(a0, n_iters, st0);
+                return Lc::rl_reg(a0, n_iters, st0);
             }
         }
         // a.o0 = x (output, also the iterate); otf kept in a.otf.  The whole iteration loop runs per
@@ -3251,7 +3241,7 @@ int gd_set_fused_init(int on) {
 
 int gd_set_fused_rl(int on) {
     const int old = g_fused_rl;
-    g_fused_rl = on == 2 ? 2 : on ? 1 : 0;
+    g_fused_rl = on ? 1 : 0;
     return old;
 }
 

@@ -17,8 +17,10 @@
 #ifndef GD_RL_SRC_EARLY
 #define GD_RL_SRC_EARLY 0  // 1: the row pass loads y / x before the row IFFT (52 VGPRs spilled: slower)
 #endif
-// OTF columns (the stored-OTF form, COTF = false): slice A's column 0 is loaded before the forward column FFTs, its
-// column 1 right after them (latency hidden; loading both before the FFTs, or slice B's too, measured slower)
+#ifndef GD_RL_HPF
+#define GD_RL_HPF 4  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden);
+                      // bit 2: slice A's column 0 before the FFTs, column 1 right after them; bit 3 (with 2): the Nyquist bins too
+#endif
 #ifndef GD_RL_DPP
 #define GD_RL_DPP 0  // 1: every line FFT transposes in registers (DPP) instead of through the LDS exchange
 #endif
@@ -37,15 +39,7 @@ __device__ __forceinline__ float rl_div(float y, float d) {
     return y / d;
 #endif
 }
-#ifndef GD_RL_COTF_ORDER
-#define GD_RL_COTF_ORDER 1
-#endif
-// COTF: the OTF is not read from HBM.  Each column's OTF is built in the kernel from the PSF's compact row spectra
-// (k_psf_rows<L, true>: h complex values per column, a.s_u1 + g K L, 4 loads per lane) and transformed there, as
-// k_gal_reg_init does (init_otf_column).  Per iteration that replaces two 264 KB OTF reads per galaxy (the stored
-// form reads H for the forward and for the adjoint convolution) with 2 x 50 KB of compact rows, which the galaxies
-// in flight keep in L2, at the price of 2 x 129 more column FFTs.  div = H(0, 0) comes from the same transform.
-template <int L, bool COTF = false>
+template <int L>
 __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
     using RG = RegGeo<L>;
     constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
@@ -56,16 +50,14 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
     __shared__ float2 nyq[RG::NP];  // X_p[L/2] of every pair
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its product
     __shared__ float nyqo[L];       // the Nyquist column after the inverse (x(., L/2))
-    __shared__ float2 nyqh[COTF ? L : 1];  // COTF: the OTF's Nyquist column
-    __shared__ float s_div;                // COTF: H(0, 0)
-    __shared__ float2 park2[COTF ? RG::PPL * RG::THREADS : 1];  // COTF: X[q][RB0 + PXB] during column A
     const int tid0 = threadIdx.x;
     const int g = blockIdx.x;
     fill_twiddles<L>(tw, tid0, T);
     const float* yg = a.y + (size_t)g * L * L;
     float* xg = a.o0 + (size_t)g * L * L;
     const float2* Hg = a.otf + (size_t)g * K * L;
-    const float div0 = COTF ? 1.f : Hg[0].x;  // conv(Ht, ones) = H(0, 0) (COTF: s_div, from iteration 0's first pass)
+    const float div = Hg[0].x;  // conv(Ht, ones) = H(0, 0)
+    const float idiv = 1.0f / div;
     const int tid = tid0;
     GD_TRACE(0);
 
@@ -161,80 +153,70 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             for (int q = 0; q < RG::PPL; ++q)
 #pragma unroll
                 for (int r = RB0; r < RB0 + RG::PXB; ++r) park[(q * RG::PXB + r - RB0) * T + tt] = X[q][r];
-            if constexpr (COTF) {  // one more slice B register per pair parked: room for the OTF column's FFT
-#pragma unroll
-                for (int q = 0; q < RG::PPL; ++q) park2[q * T + tt] = X[q][RB0 + RG::PXB];
-            }
             __builtin_amdgcn_sched_barrier(0);
-            static_assert(RG::CPL == 2, "two columns per line and slice");
-            // data column split (line 0: column 0 + i column L/2 -> column 0, nyqc)
-            auto dsplit = [&]() {
-                if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
+#if GD_RL_HPF & 1
+            float2 hA[RG::CPL][F2];  // slice A's OTF columns in flight during its forward FFTs
 #pragma unroll
-                    for (int s = 0; s < F2; ++s) my[j + F1 * s] = CA[0][s];
-                    wave_lds_sync();
-#pragma unroll
-                    for (int s = 0; s < F2; ++s) {
-                        const int ky = j + F1 * s;
-                        const float2 z = CA[0][s], zm = my[(L - ky) & (L - 1)];
-                        nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
-                        CA[0][s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-                    }
-                    wave_lds_sync();
-                }
-            };
-            if constexpr (COTF) {
-#if GD_RL_COTF_ORDER == 1
-                // per column: forward FFT, (line 0: split), the OTF column's FFT, product
-#pragma unroll
-                for (int u = 0; u < RG::CPL; ++u) {
-                    float2 h4[4];
-                    init_hload4<L>(a, h4, g, line + LINES * u, j);
-                    __builtin_amdgcn_sched_barrier(0);
-                    reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
-                    if (u == 0) dsplit();
-                    __builtin_amdgcn_sched_barrier(0);
-                    float2 Hc[F2];
-                    init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh, &h4);
-                    if (u == 0 && !CONJ && it == 0 && l0 && j == 0) s_div = Hc[0].x;
-                    happly(CA[u], Hc);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#else
-                // per column: the OTF column's FFT first, then the data column's FFT, (line 0: split), product
-#pragma unroll
-                for (int u = 0; u < RG::CPL; ++u) {
-                    float2 h4[4], Hc[F2];
-                    init_hload4<L>(a, h4, g, line + LINES * u, j);
-                    init_otf_column<L>(a, Hc, g, line + LINES * u, j, l0 && u == 0, my, tw, nyqh, &h4);
-                    if (u == 0 && !CONJ && it == 0 && l0 && j == 0) s_div = Hc[0].x;
-                    __builtin_amdgcn_sched_barrier(0);
-                    reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
-                    if (u == 0) dsplit();
-                    happly(CA[u], Hc);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+            for (int u = 0; u < RG::CPL; ++u) hload(hA[u], line + LINES * u);
+            __builtin_amdgcn_sched_barrier(0);
 #endif
-            } else {
-                float2 hA0[F2], hA1[F2];  // stored OTF: column 0 in flight during the FFTs, column 1 after them
-                hload(hA0, line);
-                __builtin_amdgcn_sched_barrier(0);
+#if GD_RL_HPF & 4
+            static_assert(RG::CPL == 2, "two columns per line and slice");
+            float2 hA0[F2];  // column 0's OTF, in flight during the FFTs
+            hload(hA0, line);
+#if GD_RL_HPF & 8
+            const bool nq = __builtin_amdgcn_readfirstlane(tt >> 6) < L / 64;
+            float2 hn4 = make_float2(0.f, 0.f);  // the Nyquist bin's OTF too
+            if (nq) hn4 = Hg[(size_t)(L / 2) * L + opaque(tt)];
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
-                for (int u = 0; u < RG::CPL; ++u) {
-                    reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                hload(hA1, line + LINES);
-                __builtin_amdgcn_sched_barrier(0);
-                dsplit();
-                happly(CA[0], hA0);
-                __builtin_amdgcn_sched_barrier(0);
-                happly(CA[1], hA1);
+            for (int u = 0; u < RG::CPL; ++u) {
+                reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            lds_barrier();  // nyqc (COTF: nyqh) complete
+#if GD_RL_HPF & 4
+            float2 hA1[F2];  // column 1's OTF, in flight during the split and column 0's products
+            hload(hA1, line + LINES);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
+#pragma unroll
+                for (int s = 0; s < F2; ++s) my[j + F1 * s] = CA[0][s];
+                wave_lds_sync();
+#pragma unroll
+                for (int s = 0; s < F2; ++s) {
+                    const int ky = j + F1 * s;
+                    const float2 z = CA[0][s], zm = my[(L - ky) & (L - 1)];
+                    nyqc[ky] = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+                    CA[0][s] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+                }
+                wave_lds_sync();
+            }
+#if GD_RL_HPF & 4
+            happly(CA[0], hA0);
+            __builtin_amdgcn_sched_barrier(0);
+            happly(CA[1], hA1);
+            __builtin_amdgcn_sched_barrier(0);
+#else
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+#if GD_RL_HPF & 1
+                happly(CA[u], hA[u]);
+#else
+                hmul(CA[u], line + LINES * u);
+#endif
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
+            lds_barrier();  // nyqc complete
             if (__builtin_amdgcn_readfirstlane(tt >> 6) < L / 64) {
-                const float2 hn = COTF ? nyqh[tt] : Hg[(size_t)(L / 2) * L + tt];
+#if GD_RL_HPF & 8
+                const float2 hn = hn4;
+#else
+                const float2 hn = Hg[(size_t)(L / 2) * L + tt];
+#endif
                 nyqc[tt] = cscale(CONJ ? cmulc(nyqc[tt], hn) : cmul(nyqc[tt], hn), inv_n);
             }
             lds_barrier();  // Nyquist products
@@ -257,10 +239,6 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             for (int q = 0; q < RG::PPL; ++q)
 #pragma unroll
                 for (int r = RB0; r < RB0 + RG::PXB; ++r) X[q][r] = park[(q * RG::PXB + r - RB0) * T + opaque(tt)];
-            if constexpr (COTF) {
-#pragma unroll
-                for (int q = 0; q < RG::PPL; ++q) X[q][RB0 + RG::PXB] = park2[q * T + opaque(tt)];
-            }
             lds_barrier();  // parked bins read -> slice B
 #pragma unroll
             for (int q = 0; q < RG::PPL; ++q) {
@@ -283,21 +261,20 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #pragma unroll
             for (int s = 0; s < F2; ++s) park[s * T + tt] = CA[RG::CPL - 1][s];
             __builtin_amdgcn_sched_barrier(0);
+#if GD_RL_HPF & 2
+            float2 hB[RG::CPL][F2];  // slice B's OTF columns in flight during its forward FFTs
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) hload(hB[u], KS + line + LINES * u);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < RG::CPL; ++u) {
-                float2 h4B[4];  // COTF: the column's compact OTF rows, in flight during its forward FFT
-                if constexpr (COTF) {
-                    init_hload4<L>(a, h4B, g, KS + line + LINES * u, j);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
                 reg_fft<L, false, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
-                if constexpr (COTF) {
-                    float2 Hc[F2];
-                    init_otf_column<L>(a, Hc, g, KS + line + LINES * u, j, false, my, tw, nyqh, &h4B);
-                    happly(CB[u], Hc);
-                } else {
-                    hmul(CB[u], KS + line + LINES * u);
-                }
+#if GD_RL_HPF & 2
+                happly(CB[u], hB[u]);
+#else
+                hmul(CB[u], KS + line + LINES * u);
+#endif
                 reg_fft<L, true, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
                 pin(CB[u]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -309,7 +286,6 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
         // (row FFT -> X); UPD: the x update and store, else the ratio
         auto rows = [&](auto updc) {
             constexpr bool UPD = decltype(updc)::value;
-            const float dv = COTF ? s_div : div0, idiv = 1.0f / dv;
             static_for<0, 2>([&](auto hfc) {
                 constexpr int hf = decltype(hfc)::value;
                 lds_barrier();  // parked results / exchange areas -> row half spectra
@@ -366,7 +342,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                         if constexpr (UPD) {
                             // x * numerator / divisor
                             V[r] = GD_RL_FASTDIV ? make_float2(src[r].x * V[r].x * idiv, src[r].y * V[r].y * idiv)
-                                                 : make_float2(src[r].x * V[r].x / dv, src[r].y * V[r].y / dv);
+                                                 : make_float2(src[r].x * V[r].x / div, src[r].y * V[r].y / div);
                             xg[ro0 + F1 * r] = V[r].x;
                             xg[ro0 + L + F1 * r] = V[r].y;
                         } else {

@@ -125,8 +125,7 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
 int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
               long long alpha_stride, float* x, int N, int H, int W, void* ws, void* stream);
 
-/* Richardson-Lucy from x0 = max(y,0); otf_half (gd_otf_bytes) is scratch for the OTF: it receives the OTF,
- * or at 256^2 with a PSF side <= 64 (gd_set_fused_rl) the PSF's compact row spectra only. */
+/* Richardson-Lucy from x0 = max(y,0); otf_half receives the OTF (gd_otf_bytes). */
 int gd_richardson_lucy(const float* y, const float* psf, long long psf_gstride, int h, int w, int n_iters,
                        float* x, int N, int H, int W, void* otf_half, void* ws, void* stream);
 
@@ -233,11 +232,10 @@ int gd_set_capture_pipeline(int mode);
 int gd_set_fused_iteration(int on);
 
 /* Richardson-Lucy at 256^2 (gd_richardson_lucy, models/Richard_Lucy.py:10-24): on = 1 (default) runs the
- * whole n_iters loop of each galaxy inside one 512-thread workgroup (k_rl_reg: the galaxy's spectra stay
- * on-chip; x and y are re-read from the cache hierarchy) with every OTF column built in the kernel from the
- * PSF's compact row spectra (PSF side <= 64; larger PSFs take on = 2's form); 2 = the same loop reading the
- * OTF computed beforehand; 0 selects the chunked chain (four launches per iteration through the workspace).
- * Returns the previous setting; process-wide. */
+ * OTF, then the whole n_iters loop of each galaxy inside one 512-thread workgroup (k_rl_reg: the
+ * galaxy's spectra stay on-chip; x, y and the OTF are re-read from the cache hierarchy); 0 selects the
+ * chunked chain (four launches per iteration through the workspace).  Returns the previous setting;
+ * process-wide. */
 int gd_set_fused_rl(int on);
 
 /* SubNet from the PSFs (gd_subnet_rhos_psf): batches of at most n galaxies run features + MLP in ONE

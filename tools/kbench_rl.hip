@@ -2,8 +2,6 @@
 // and a positive Gaussian-like PSF per galaxy; the OTF through the engine's gd_psf_to_otf.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 [-DGD_FUSED_TRACE=1] -o tools/kbench_rl tools/kbench_rl.hip
 //   tools/kbench_rl [N=4096] [n_iters=100] [reps=3]
-// Times both forms: the stored OTF (k_rl_reg<256, false>) and the OTF built in the kernel from the PSF's compact
-// row spectra (k_psf_rows<256, true> + k_rl_reg<256, true>), and compares their outputs.
 #include "../galaxy-deconv_amd/csrc/gd_engine.hip"
 
 #include <cstdlib>
@@ -29,9 +27,8 @@ __global__ void k_psf(float* p, int N, int h) {
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 100, reps = argc > 3 ? atoi(argv[3]) : 3;
     constexpr int L = 256, h = 48;
-    float *y, *x, *x2, *psf; void *otf, *otf2, *ws;
+    float *y, *x, *psf; void *otf, *ws;
     CK(hipMalloc(&y, (size_t)N * L * L * 4)); CK(hipMalloc(&x, (size_t)N * L * L * 4));
-    CK(hipMalloc(&x2, (size_t)N * L * L * 4)); CK(hipMalloc(&otf2, gd_otf_bytes(N, L, L)));
     CK(hipMalloc(&psf, (size_t)N * h * h * 4));
     CK(hipMalloc(&otf, gd_otf_bytes(N, L, L))); CK(hipMalloc(&ws, gd_workspace_bytes(N, L, L)));
     hipLaunchKernelGGL(k_img, dim3(4096), dim3(256), 0, 0, y, (size_t)N * L * L, 1u);
@@ -58,35 +55,6 @@ int main(int argc, char** argv) {
     ms /= reps;
     printf("k_rl_reg<256> N=%d n_iters=%d  %.3f ms  %.0f gal/s  %.2f us per galaxy-iteration-round\n", N, n, ms,
            N / (ms * 1e-3), ms * 1e3 / (n * ((N + 255) / 256)));
-    {
-        Args c = a;
-        c.o0 = x2; c.psf = psf; c.psf_gstride = h * h; c.h = h; c.s_u1 = reinterpret_cast<float2*>(otf2);
-        const int bpg = (h / 2 + Geo<L>::LPB - 1) / Geo<L>::LPB;
-        auto run = [&]() {
-            hipLaunchKernelGGL((k_psf_rows<L, true>), dim3(N * bpg), dim3(256), 0, 0, c);
-            hipLaunchKernelGGL((k_rl_reg<L, true>), dim3(N), dim3(512), 0, 0, c, n);
-        };
-        run();
-        CK(hipGetLastError()); CK(hipDeviceSynchronize());
-        CK(hipEventRecord(e0));
-        for (int r = 0; r < reps; ++r) run();
-        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-        float ms2; CK(hipEventElapsedTime(&ms2, e0, e1));
-        ms2 /= reps;
-        printf("k_psf_rows<256,STATE> + k_rl_reg<256,COTF> N=%d n_iters=%d  %.3f ms  %.0f gal/s  (%.3f x the stored-OTF form)\n",
-               N, n, ms2, N / (ms2 * 1e-3), ms2 / ms);
-        const size_t cnt = (size_t)(N < 64 ? N : 64) * L * L;
-        std::vector<float> h1(cnt), h2(cnt);
-        CK(hipMemcpy(h1.data(), x, cnt * 4, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(h2.data(), x2, cnt * 4, hipMemcpyDeviceToHost));
-        double num = 0, den = 0, mx = 0;
-        for (size_t i = 0; i < cnt; ++i) {
-            const double d = (double)h1[i] - h2[i];
-            num += d * d; den += (double)h1[i] * h1[i];
-            mx = std::max(mx, std::fabs(d) / (std::fabs((double)h1[i]) + 1e-30));
-        }
-        printf("COTF vs stored OTF (first %zu galaxies): normwise %.3e, max rel %.3e\n", cnt / (L * L), std::sqrt(num / den), mx);
-    }
     std::vector<float> hx(L * L);
     CK(hipMemcpy(hx.data(), x, L * L * 4, hipMemcpyDeviceToHost));
     double s = 0; bool fin = true;

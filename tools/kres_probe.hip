@@ -11,8 +11,7 @@ int main(int argc, char**) {
         hipLaunchKernelGGL((gd::k_gal_reg_init<256, false>), dim3(1), dim3(512), 0, 0, a);
         hipLaunchKernelGGL((gd::k_gal_reg_init<256, true>), dim3(1), dim3(512), 0, 0, a);
         hipLaunchKernelGGL((gd::k_pois_b<256>), dim3(1), dim3(512), 0, 0, a, 0);
-        hipLaunchKernelGGL((gd::k_rl_reg<256, false>), dim3(1), dim3(512), 0, 0, a, 1);
-        hipLaunchKernelGGL((gd::k_rl_reg<256, true>), dim3(1), dim3(512), 0, 0, a, 1);
+        hipLaunchKernelGGL((gd::k_rl_reg<256>), dim3(1), dim3(512), 0, 0, a, 1);
     }
     return 0;
 }
