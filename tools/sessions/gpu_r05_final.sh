@@ -1,14 +1,10 @@
-# Round-5 final check, part 1 (tag = $1): Poisson pass-A A/B (spill fix), GPU tests + smoke, PMC traffic
+# Round-5 final check, part 1 (tag = $1): GPU tests + smoke, PMC traffic
 # (FETCH_SIZE / WRITE_SIZE in separate passes) for the default / Poisson / RL / 48^2 workloads of the final
 # engine rev, rocprofv3 kernel stats of the default bench and the 48^2 line, pmc_summary -> pmc_traffic_*.json.
 # Part 2 (gpu_r05_benchfinal.sh) runs the bench lines reading that traffic.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; export TMPDIR=/tmp; T=${1:-r05final}; mkdir -p $O
 B="python3 $R/bench.py --no-cpu-baseline --no-e2e --no-graph --no-ingest --no-extra"
-cd $R && for round in 1 2 3; do for b in kbench_pois_spill kbench_pois; do
-  echo "=== $b round $round" >> $O/abpois_$T.txt
-  timeout -k 10 120 tools/bin/$b 4096 20 >> $O/abpois_$T.txt 2>&1 || exit 1
-done; done &&
-GD_PARITY_LOG=$O/parity_$T.jsonl timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
+cd $R && GD_PARITY_LOG=$O/parity_$T.jsonl timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$T.txt 2>&1 &&
 cd /tmp && timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "gd::" -d $O/pf_$T -o fetch --output-format csv -- $B --steps 1 --warmup 1 > /dev/null 2> $O/pmc_$T.err &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "gd::" -d $O/pw_$T -o write --output-format csv -- $B --steps 1 --warmup 1 > /dev/null 2>> $O/pmc_$T.err &&
