@@ -567,6 +567,8 @@ def measure(args, ctx):
         tgr, teag = sorted(tgs)[1], sorted(teg)[1]
         graphed = {"value": N * world * args.steps / tgr, "unit": "galaxies/s", "ms_per_step": tgr * 1e3 / args.steps,
                    "eager_interleaved": {"value": N * world * args.steps / teag, "ms_per_step": teag * 1e3 / args.steps},
+                   "blocks_ms_per_step": {"eager": [round(t * 1e3 / args.steps, 4) for t in teg],
+                                          "graphed": [round(t * 1e3 / args.steps, 4) for t in tgs]},
                    "note": "medians of 3 interleaved blocks of K eager / K replayed steps (no per-op profiling events)",
                    "bit_identical_to_eager": bool(torch.equal(gout, out))}
         del gf, gout
