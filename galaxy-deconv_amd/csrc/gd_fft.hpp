@@ -541,4 +541,75 @@ __device__ __forceinline__ void line_fft(float2 (&v)[Plan<L>::F2], int j, float2
     wave_lds_sync();  // the area may be rewritten by the next line_fft of this wave
 }
 
+// Two independent line FFTs of one line (F1 = F2 = 16), the same arithmetic as two line_fft<L, INV, LEAN> calls
+// (bit-identical results) through ONE exchange area, interleaved so that each transform's LDS round trip is
+// covered by the other's register work: stage A of v0, its exchange write and read issue; stage A of v1 while
+// those reads are in flight; v1's exchange write (LDS requests of a wave are processed in order, so it lands
+// after v0's reads); stage B of v0 while v1's reads are in flight; stage B of v1.  The twiddles are formed once.
+template <int L, bool INV, bool LEAN = false>
+__device__ __forceinline__ void line_fft2(float2 (&v0)[Plan<L>::F2], float2 (&v1)[Plan<L>::F2], int j, float2* xch,
+                                          const float2* tw) {
+    constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, LD = F2 + 1;
+    static_assert(F1 == 16 && F2 == 16, "paired line FFTs are for 16 x 16 lines");
+    c2 w[F2], t[F2];
+    if constexpr (LEAN) {
+        c2 t1[4], t4[4];
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+            t1[i] = tc2(tw[j * i]);
+            t4[i] = tc2(tw[4 * j * i]);
+        }
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            const int a = k1 & 3, b = k1 >> 2;
+            if (a != 0 && b != 0) t[k1] = pmul_t(t4[b], t1[a]);
+        }
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) {
+            const int a = k1 & 3, b = k1 >> 2;
+            w[k1] = a == 0 ? t4[b] : (b == 0 ? t1[a] : pmul_r<false>(t4[b], t1[a], t[k1]));
+        }
+    } else {
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) w[k1] = tc2(tw[j * k1]);
+    }
+    auto stage_a = [&](float2 (&v)[F2]) {
+        c2 x[F2];
+#pragma unroll
+        for (int i = 0; i < F2; ++i) x[i] = tc2(v[i]);
+        DFT<F2, INV>::run(x);
+        c2 u[F2];
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) u[k1] = pmul_t(x[k1], w[k1]);
+#pragma unroll
+        for (int k1 = 1; k1 < F2; ++k1) x[k1] = pmul_r<INV>(x[k1], w[k1], u[k1]);
+#pragma unroll
+        for (int k1 = 0; k1 < F2; ++k1) v[k1] = tf2(x[k1]);
+    };
+    auto stage_b = [&](float2 (&v)[F2]) {
+        c2 z[F1];
+#pragma unroll
+        for (int n1 = 0; n1 < F1; ++n1) z[n1] = tc2(v[n1]);
+        DFT<F1, INV>::run(z);
+#pragma unroll
+        for (int k2 = 0; k2 < F1; ++k2) v[k2] = tf2(z[k2]);
+    };
+    stage_a(v0);
+#pragma unroll
+    for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v0[k1];
+    wave_lds_sync();
+#pragma unroll
+    for (int n1 = 0; n1 < F1; ++n1) v0[n1] = xch[n1 * LD + j];
+    stage_a(v1);
+    wave_lds_sync();  // (program order: v0's reads before v1's writes to the same area)
+#pragma unroll
+    for (int k1 = 0; k1 < F2; ++k1) xch[j * LD + k1] = v1[k1];
+    wave_lds_sync();
+#pragma unroll
+    for (int n1 = 0; n1 < F1; ++n1) v1[n1] = xch[n1 * LD + j];
+    stage_b(v0);
+    stage_b(v1);
+    wave_lds_sync();  // the area may be rewritten by the next line_fft of this wave
+}
+
 }  // namespace gd

@@ -300,6 +300,15 @@ __device__ __forceinline__ void reg_fft(float2 (&v)[16], int j, float2* xch, con
     line_fft<L, INV, GD_REG_LEAN != 0, DPP>(v, j, xch, tw);
 #endif
 }
+// two independent lines' transforms interleaved through one exchange area (line_fft2; bit-identical to two reg_fft)
+template <int L, bool INV>
+__device__ __forceinline__ void reg_fft2(float2 (&v0)[16], float2 (&v1)[16], int j, float2* xch, const float2* tw) {
+#if GD_REG_NOFFT
+    asm volatile("" ::: "memory");
+#else
+    line_fft2<L, INV, GD_REG_LEAN != 0>(v0, v1, j, xch, tw);
+#endif
+}
 
 #ifndef GD_REG_SLD_PAD
 #define GD_REG_SLD_PAD 1

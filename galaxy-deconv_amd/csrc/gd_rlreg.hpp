@@ -14,15 +14,15 @@
 // The OTF (a.otf, [N][K][L], ky contiguous) is computed beforehand (psf_to_otf).
 // Included inside namespace gd by gd_engine.hip (after gd_galreg.hpp).
 
-#ifndef GD_RL_SRC_EARLY
-#define GD_RL_SRC_EARLY 0  // 1: the row pass loads y / x before the row IFFT (52 VGPRs spilled: slower)
-#endif
 #ifndef GD_RL_HPF
 #define GD_RL_HPF 4  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden);
                       // bit 2: slice A's column 0 before the FFTs, column 1 right after them; bit 3 (with 2): the Nyquist bins too
 #endif
 #ifndef GD_RL_DPP
 #define GD_RL_DPP 0  // 1: every line FFT transposes in registers (DPP) instead of through the LDS exchange
+#endif
+#ifndef GD_RL_PAIR
+#define GD_RL_PAIR 3  // bit 0: slice A's two columns transformed as a pair (reg_fft2), bit 1: slice B's, bit 2: the rows
 #endif
 #ifndef GD_RL_FASTDIV
 #define GD_RL_FASTDIV 1
@@ -171,10 +171,15 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #endif
             __builtin_amdgcn_sched_barrier(0);
 #endif
-#pragma unroll
-            for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
+            if constexpr ((GD_RL_PAIR & 1) != 0) {
+                reg_fft2<L, false>(CA[0], CA[1], opaque(j), my, tw);
                 __builtin_amdgcn_sched_barrier(0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < RG::CPL; ++u) {
+                    reg_fft<L, false, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
 #if GD_RL_HPF & 4
             float2 hA1[F2];  // column 1's OTF, in flight during the split and column 0's products
@@ -225,11 +230,18 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                 const float2 cn = nyqc[j + F1 * s];
                 if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
             }
-#pragma unroll
-            for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, true, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
-                pin(CA[u]);  // the column results materialised here (spill-free register allocation)
+            if constexpr ((GD_RL_PAIR & 1) != 0) {
+                reg_fft2<L, true>(CA[0], CA[1], opaque(j), my, tw);
+                pin(CA[0]);
+                pin(CA[1]);
                 __builtin_amdgcn_sched_barrier(0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < RG::CPL; ++u) {
+                    reg_fft<L, true, GD_RL_DPP != 0>(CA[u], opaque(j), my, tw);
+                    pin(CA[u]);  // the column results materialised here (spill-free register allocation)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
             if (l0) {
 #pragma unroll
@@ -267,17 +279,27 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             for (int u = 0; u < RG::CPL; ++u) hload(hB[u], KS + line + LINES * u);
             __builtin_amdgcn_sched_barrier(0);
 #endif
+            if constexpr ((GD_RL_PAIR & 2) != 0) {
+                reg_fft2<L, false>(CB[0], CB[1], opaque(j), my, tw);
 #pragma unroll
-            for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, false, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
-#if GD_RL_HPF & 2
-                happly(CB[u], hB[u]);
-#else
-                hmul(CB[u], KS + line + LINES * u);
-#endif
-                reg_fft<L, true, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
-                pin(CB[u]);
+                for (int u = 0; u < RG::CPL; ++u) hmul(CB[u], KS + line + LINES * u);
+                reg_fft2<L, true>(CB[0], CB[1], opaque(j), my, tw);
+                pin(CB[0]);
+                pin(CB[1]);
                 __builtin_amdgcn_sched_barrier(0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < RG::CPL; ++u) {
+                    reg_fft<L, false, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
+#if GD_RL_HPF & 2
+                    happly(CB[u], hB[u]);
+#else
+                    hmul(CB[u], KS + line + LINES * u);
+#endif
+                    reg_fft<L, true, GD_RL_DPP != 0>(CB[u], opaque(j), my, tw);
+                    pin(CB[u]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
 #pragma unroll
             for (int s = 0; s < F2; ++s) CA[RG::CPL - 1][s] = park[s * T + opaque(tt)];
@@ -322,21 +344,13 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                     }
                 }
                 lds_barrier();  // row half spectra -> exchange areas
-#pragma unroll
-                for (int w = 0; w < RG::HPL; ++w) {
-                    float2 (&V)[F2] = X[2 * hf + w];
+                // the pointwise step of row pair w (V = X[2 hf + w], already inverse-transformed)
+                auto pointwise = [&](float2 (&V)[F2], int w) {
                     const size_t ro0 = (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
                     float2 src[F2];  // (row e, row o) pixels: y (ratio), x (update)
                     const float* sp = (UPD ? xg : yg) + ro0;
-                    if (GD_RL_SRC_EARLY) {
 #pragma unroll
-                        for (int r = 0; r < F2; ++r) src[r] = make_float2(sp[F1 * r], sp[L + F1 * r]);
-                    }
-                    reg_fft<L, true, GD_RL_DPP != 0>(V, opaque(j), my, tw);
-                    if (!GD_RL_SRC_EARLY) {
-#pragma unroll
-                        for (int r = 0; r < F2; ++r) src[r] = make_float2(sp[F1 * r], sp[L + F1 * r]);
-                    }
+                    for (int r = 0; r < F2; ++r) src[r] = make_float2(sp[F1 * r], sp[L + F1 * r]);
 #pragma unroll
                     for (int r = 0; r < F2; ++r) {
                         if constexpr (UPD) {
@@ -349,9 +363,29 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                             V[r] = make_float2(rl_div(fmaxf(src[r].x, 0.f), V[r].x), rl_div(fmaxf(src[r].y, 0.f), V[r].y));  // y / Hx
                         }
                     }
-                    if (!(UPD && last)) reg_fft<L, false, GD_RL_DPP != 0>(V, opaque(j), my, tw);
-                    pin(V);
+                };
+                if constexpr ((GD_RL_PAIR & 4) != 0) {
+                    static_assert(RG::HPL == 2, "two row pairs per line and half");
+                    reg_fft2<L, true>(X[2 * hf], X[2 * hf + 1], opaque(j), my, tw);
                     __builtin_amdgcn_sched_barrier(0);
+                    pointwise(X[2 * hf], 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    pointwise(X[2 * hf + 1], 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (!(UPD && last)) reg_fft2<L, false>(X[2 * hf], X[2 * hf + 1], opaque(j), my, tw);
+                    pin(X[2 * hf]);
+                    pin(X[2 * hf + 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                } else {
+#pragma unroll
+                    for (int w = 0; w < RG::HPL; ++w) {
+                        float2 (&V)[F2] = X[2 * hf + w];
+                        reg_fft<L, true, GD_RL_DPP != 0>(V, opaque(j), my, tw);
+                        pointwise(V, w);
+                        if (!(UPD && last)) reg_fft<L, false, GD_RL_DPP != 0>(V, opaque(j), my, tw);
+                        pin(V);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
             });
         };

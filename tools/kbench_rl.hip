@@ -60,6 +60,14 @@ int main(int argc, char** argv) {
     double s = 0; bool fin = true;
     for (float v : hx) { s += v; fin = fin && std::isfinite(v); }
     printf("galaxy 0: sum %.6e finite %d\n", s, (int)fin);
+    {  // FNV-1a over the first min(N, 64) galaxies' outputs (bitwise comparison across builds)
+        const size_t cnt = (size_t)(N < 64 ? N : 64) * L * L;
+        std::vector<unsigned> hb(cnt);
+        CK(hipMemcpy(hb.data(), x, cnt * 4, hipMemcpyDeviceToHost));
+        unsigned long long hsh = 1469598103934665603ull;
+        for (unsigned v : hb) { hsh ^= v; hsh *= 1099511628211ull; }
+        printf("output fnv %016llx (first %zu galaxies)\n", hsh, cnt / (L * L));
+    }
 #if GD_FUSED_TRACE
     std::vector<unsigned long long> t((size_t)N * 16);
     CK(hipMemcpy(t.data(), tr, t.size() * 8, hipMemcpyDeviceToHost));
