@@ -214,6 +214,10 @@ __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb,
 }
 // GD_REG_SPF: the first D groups of a slice's state are loaded BEFORE the slice's forward column FFTs
 // (fused_prefetch4x), so their latency runs under the transforms instead of opening the update
+#ifndef GD_REG_PAIR
+#define GD_REG_PAIR 3  // k_gal_reg (Gaussian): bit 0: a slice's two forward column transforms as an interleaved pair
+                       // (reg_fft2), bit 1: the inverse ones
+#endif
 #ifndef GD_REG_SPF
 #define GD_REG_SPF 1
 #endif
@@ -470,11 +474,16 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     constexpr bool SPF = GD_REG_SPF && !POIS;
     SGroup preA[DPT];
     if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preA, g, line, LINES, j, first, last);
-#pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) {
-        reg_fft<L, false>(CA[u], opaque(j), my, tw);
-        if (GD_REG_PINF) pin(CA[u]);
+    if constexpr ((GD_REG_PAIR & 1) != 0 && !POIS) {
+        reg_fft2<L, false>(CA[0], CA[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) {
+            reg_fft<L, false>(CA[u], opaque(j), my, tw);
+            if (GD_REG_PINF) pin(CA[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     if (l0) {
 #pragma unroll
@@ -500,6 +509,10 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         const float2 cn = nyqc[j + F1 * s];
         if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
     }
+    if constexpr ((GD_REG_PAIR & 2) != 0 && !POIS) {
+        reg_fft2<L, true>(CA[0], CA[1], opaque(j), my, tw);
+        __builtin_amdgcn_sched_barrier(0);
+    } else
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CA[u], opaque(j), my, tw);
@@ -544,13 +557,22 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     GD_TRACE(6);
     SGroup preB[DPT];
     if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preB, g, KS + line, LINES, j, first, last);
-#pragma unroll
-    for (int u = 0; u < RG::CPL; ++u) {
-        reg_fft<L, false>(CB[u], opaque(j), my, tw);
-        if (GD_REG_PINF) pin(CB[u]);
+    if constexpr ((GD_REG_PAIR & 1) != 0 && !POIS) {
+        reg_fft2<L, false>(CB[0], CB[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+        for (int u = 0; u < RG::CPL; ++u) {
+            reg_fft<L, false>(CB[u], opaque(j), my, tw);
+            if (GD_REG_PINF) pin(CB[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     fused_update4x<L, RG::CPL, POIS, DPT, SPF>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last, &preB);
+    if constexpr ((GD_REG_PAIR & 2) != 0 && !POIS) {
+        reg_fft2<L, true>(CB[0], CB[1], opaque(j), my, tw);
+        __builtin_amdgcn_sched_barrier(0);
+    } else
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CB[u], opaque(j), my, tw);
@@ -736,6 +758,10 @@ __device__ __forceinline__ void init_otf_column(const Args& a, float2 (&Hc)[16],
 #ifndef GD_INIT_DPP
 #define GD_INIT_DPP 0  // 1: the init's line FFTs transpose in registers (DPP) instead of through the LDS exchange
 #endif
+#ifndef GD_INIT_PAIR
+#define GD_INIT_PAIR 1  // bit 0: a slice's two data columns transformed as an interleaved pair (reg_fft2), bit 1: the
+                        // phase I rows
+#endif
 // POIS: the Poisson two-pass init (k_gal_reg_init<L, true>): the same init_l2 and F(x0), but the OTF
 // itself goes to the G slot (the Poisson V step reads y, not G); pass B then forms w1 and W~1.
 template <int L, bool POIS = false>
@@ -827,11 +853,20 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int u = 0; u < RG::CPL; ++u) init_hload4<L>(a, hpA[u], g, line + LINES * u, j);
             __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int u = 0; u < RG::CPL; ++u) {
-            reg_fft<L, false, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
-            if (POIS) pin(CA[u]);
+        if constexpr ((GD_INIT_PAIR & 1) != 0 && !POIS) {  // (the Poisson init spills with it)
+            reg_fft2<L, false>(CA[0], CA[1], opaque(j), my, tw);
+            if (POIS) {
+                pin(CA[0]);
+                pin(CA[1]);
+            }
             __builtin_amdgcn_sched_barrier(0);
+        } else {
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                reg_fft<L, false, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
+                if (POIS) pin(CA[u]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         if (l0) {  // column 0 / Nyquist column split (the exchange area is free: the FFTs are done)
 #pragma unroll
@@ -864,11 +899,20 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 const float2 cn = nyqc[j + F1 * s];
                 if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
             }
-#pragma unroll
-            for (int u = 0; u < RG::CPL; ++u) {
-                reg_fft<L, true, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
-                if (POIS) pin(CA[u]);  // the Poisson init: materialised here, spill-free
+            if constexpr ((GD_INIT_PAIR & 1) != 0 && !POIS) {  // (the Poisson init spills with it)
+                reg_fft2<L, true>(CA[0], CA[1], opaque(j), my, tw);
+                if (POIS) {
+                    pin(CA[0]);
+                    pin(CA[1]);
+                }
                 __builtin_amdgcn_sched_barrier(0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < RG::CPL; ++u) {
+                    reg_fft<L, true, GD_INIT_DPP != 0>(CA[u], opaque(j), my, tw);
+                    if (POIS) pin(CA[u]);  // the Poisson init: materialised here, spill-free
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
             if (l0) {
 #pragma unroll
@@ -917,10 +961,15 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int u = 0; u < RG::CPL; ++u) init_hload4<L>(a, hpB[u], g, KS + line + LINES * u, j);
             __builtin_amdgcn_sched_barrier(0);
         }
-#pragma unroll
-        for (int u = 0; u < RG::CPL; ++u) {
-            reg_fft<L, false, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
+        if constexpr ((GD_INIT_PAIR & 1) != 0 && !POIS) {  // (the Poisson init spills with it)
+            reg_fft2<L, false>(CB[0], CB[1], opaque(j), my, tw);
             __builtin_amdgcn_sched_barrier(0);
+        } else {
+#pragma unroll
+            for (int u = 0; u < RG::CPL; ++u) {
+                reg_fft<L, false, GD_INIT_DPP != 0>(CB[u], opaque(j), my, tw);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
@@ -984,10 +1033,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             }
         }
         lds_barrier();  // row half spectra -> exchange areas
-#pragma unroll
-        for (int w = 0; w < RG::HPL; ++w) {
-            float2 (&V)[F2] = X[2 * hf + w];
-            reg_fft<L, true, GD_INIT_DPP != 0>(V, opaque(j), my, tw);
+        auto clamp_store = [&](float2 (&V)[F2], int w) {
             float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
 #pragma unroll
             for (int r = 0; r < F2; ++r) {  // x0 = torch.clamp(x0, 0, 1) (RIF_CLAMP)
@@ -995,9 +1041,26 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
                 o[F1 * r] = V[r].x;
                 o[L + F1 * r] = V[r].y;
             }
-            reg_fft<L, false, GD_INIT_DPP != 0>(V, opaque(j), my, tw);  // F(x0) rows
-            pin(V);
+        };
+        if constexpr ((GD_INIT_PAIR & 2) != 0) {
+            static_assert(RG::HPL == 2, "two row pairs per line and half");
+            reg_fft2<L, true>(X[2 * hf], X[2 * hf + 1], opaque(j), my, tw);
+            clamp_store(X[2 * hf], 0);
+            clamp_store(X[2 * hf + 1], 1);
+            reg_fft2<L, false>(X[2 * hf], X[2 * hf + 1], opaque(j), my, tw);  // F(x0) rows
+            pin(X[2 * hf]);
+            pin(X[2 * hf + 1]);
             __builtin_amdgcn_sched_barrier(0);
+        } else {
+#pragma unroll
+            for (int w = 0; w < RG::HPL; ++w) {
+                float2 (&V)[F2] = X[2 * hf + w];
+                reg_fft<L, true, GD_INIT_DPP != 0>(V, opaque(j), my, tw);
+                clamp_store(V, w);
+                reg_fft<L, false, GD_INIT_DPP != 0>(V, opaque(j), my, tw);  // F(x0) rows
+                pin(V);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
     });
 

@@ -242,6 +242,20 @@ int main(int argc, char** argv) {
         CK(hipGetLastError());
         const double gi = N * (2 * img_b + 2.5 * half_b + 2.0 * h * K * 8) / 1e9;
         printf("k_psf_rows<STATE> N=%d  %.3f ms; + k_gal_reg_init %.3f ms  %.2f TB/s algorithmic (%.2f GB)\n", N, mr, mi, gi / mi, gi);
+        {  // FNV-1a of the init's outputs (zin, W~, G) over the first min(N, 64) galaxies: bitwise comparison across builds
+            CK(hipDeviceSynchronize());
+            const int ng = N < 64 ? N : 64;
+            unsigned long long hsh = 1469598103934665603ull;
+            auto fold = [&](const void* p, size_t words) {
+                std::vector<unsigned> hb(words);
+                CK(hipMemcpy(hb.data(), p, words * 4, hipMemcpyDeviceToHost));
+                for (unsigned v : hb) { hsh ^= v; hsh *= 1099511628211ull; }
+            };
+            fold(b.o2, (size_t)ng * L * L);
+            fold(b.s_w, (size_t)ng * K * L * 2);
+            fold(b.s_g, (size_t)ng * K * L * 2);
+            printf("init outputs fnv %016llx (first %d galaxies)\n", hsh, ng);
+        }
 #if GD_FUSED_TRACE
         const char* inames[] = {"start -> y loaded", "row FFTs", "A gather + park", "A: Y, OTF cols, update, IFFT",
                                 "B gather", "B: Y, OTF cols, update, IFFT", "I half 0", "I half 1 (+ x0 row FFTs)",
