@@ -218,6 +218,12 @@ __device__ __forceinline__ void sgroup_load(const Args& a, SGroup& G, size_t gb,
 #define GD_REG_PAIR 3  // k_gal_reg (Gaussian): bit 0: a slice's two forward column transforms as an interleaved pair
                        // (reg_fft2), bit 1: the inverse ones
 #endif
+#ifndef GD_POIS_PAIR
+#define GD_POIS_PAIR 0  // GD_REG_PAIR for Poisson pass A as well
+#endif
+#ifndef GD_POIS_SPF
+#define GD_POIS_SPF 1  // the same for Poisson pass A (234 VGPRs with it, 248 without; pass A 1.530 -> 1.508 ms)
+#endif
 #ifndef GD_REG_SPF
 #define GD_REG_SPF 1
 #endif
@@ -471,10 +477,10 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     __builtin_amdgcn_sched_barrier(0);
     GD_TRACE(3);
     constexpr int DPT = POIS ? GD_POIS_DEPTH : GD_REG_DEPTH;
-    constexpr bool SPF = GD_REG_SPF && !POIS;
+    constexpr bool SPF = GD_REG_SPF && (!POIS || GD_POIS_SPF);
     SGroup preA[DPT];
     if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preA, g, line, LINES, j, first, last);
-    if constexpr ((GD_REG_PAIR & 1) != 0 && !POIS) {
+    if constexpr ((GD_REG_PAIR & 1) != 0 && (!POIS || GD_POIS_PAIR)) {
         reg_fft2<L, false>(CA[0], CA[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         const float2 cn = nyqc[j + F1 * s];
         if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
     }
-    if constexpr ((GD_REG_PAIR & 2) != 0 && !POIS) {
+    if constexpr ((GD_REG_PAIR & 2) != 0 && (!POIS || GD_POIS_PAIR)) {
         reg_fft2<L, true>(CA[0], CA[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
     } else
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     GD_TRACE(6);
     SGroup preB[DPT];
     if constexpr (SPF) fused_prefetch4x<L, RG::CPL, POIS, DPT>(a, preB, g, KS + line, LINES, j, first, last);
-    if constexpr ((GD_REG_PAIR & 1) != 0 && !POIS) {
+    if constexpr ((GD_REG_PAIR & 1) != 0 && (!POIS || GD_POIS_PAIR)) {
         reg_fft2<L, false>(CB[0], CB[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -569,7 +575,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
         }
     }
     fused_update4x<L, RG::CPL, POIS, DPT, SPF>(a, CB, g, KS + line, LINES, j, r1, r2, r2n, first, last, &preB);
-    if constexpr ((GD_REG_PAIR & 2) != 0 && !POIS) {
+    if constexpr ((GD_REG_PAIR & 2) != 0 && (!POIS || GD_POIS_PAIR)) {
         reg_fft2<L, true>(CB[0], CB[1], opaque(j), my, tw);
         __builtin_amdgcn_sched_barrier(0);
     } else
