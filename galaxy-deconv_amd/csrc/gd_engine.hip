@@ -2848,7 +2848,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r05.4"; }
+const char* gd_engine_rev(void) { return "r05.5"; }
 
 // the source hash __graft_entry__.build() computed (gdeconv._lib.source_hash); the "gdsrc:" marker lets the
 // build find it in the binary without loading it
@@ -2921,10 +2921,18 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream) {
     return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::irfft2(a, (hipStream_t)stream); });
 }
 
+// Gap between the Gaussian state's slots at 256^2 (bytes).  The slots are N K L complex apart, a multiple of 8 MiB
+// at 256^2 (N = 4096: 2^30 + 2^23 bytes), so one galaxy's |H|^2, G, U1 and W~ bins, which k_gal_reg streams
+// together, sat at the same offset modulo every HBM interleave period; 256 KiB between the slots spreads them
+// (tools/kbench_reg.hip KB_PAD in the engine layout: MID 1.597 -> 1.565-1.575 ms, profiles/r05_place_ab.txt).
+constexpr size_t kStateSlotGap = 256 * 1024;
+inline size_t state_slot_gap(int H, int W, int llh) { return (llh == GD_LLH_GAUSSIAN && H == 256 && W == 256) ? kStateSlotGap : 0; }
+
 size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
     if (!gd_supported_size(H, W) || N <= 0) return 0;
     const size_t spec = (size_t)N * (W / 2 + 1) * H * sizeof(float2), img = (size_t)N * H * W * sizeof(float);
-    if (llh == GD_LLH_GAUSSIAN) return (spec / 8 + 1) / 2 * 8 + 3 * spec;  // |H|^2 padded to 8-byte alignment
+    if (llh == GD_LLH_GAUSSIAN)  // |H|^2 padded to 8-byte alignment, the slot gaps
+        return (spec / 8 + 1) / 2 * 8 + 3 * spec + 3 * state_slot_gap(H, W, llh);
     // Poisson: [otf | u1 | w] (three-kernel chain); at 256^2 also room for the two-pass layout
     // [(|H|^2) | H | U1 | F(w) | H X] + w (bind_state picks the layout from gd_set_fused_iteration)
     return (H == 256 && W == 256) ? std::max(spec + 2 * img, spec / 2 + 4 * spec + img) : spec + 2 * img;
@@ -2932,7 +2940,8 @@ size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
 
 namespace {
 bool pois_two_pass(int H, int W, int llh) { return llh == GD_LLH_POISSON && H == 256 && W == 256 && g_fused != 0; }
-// state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral);
+// state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral; at 256^2 with
+// kStateSlotGap bytes between the slots);
 // Poisson: [otf | u1 | w]
 void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H;
@@ -2948,11 +2957,12 @@ void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
         return;
     }
     if (llh == GD_LLH_GAUSSIAN) {
+        const size_t gap = state_slot_gap(H, W, llh) / sizeof(float2);
         a.s_hh = reinterpret_cast<float*>(base);
-        float2* c = base + (spec + 1) / 2;  // |H|^2: spec floats, rounded up to whole float2
+        float2* c = base + (spec + 1) / 2 + gap;  // |H|^2: spec floats, rounded up to whole float2
         a.s_g = c;
-        a.s_u1 = c + spec;
-        a.s_w = c + 2 * spec;
+        a.s_u1 = c + spec + gap;
+        a.s_w = c + 2 * (spec + gap);
     } else {
         a.otf = base;
         float* u1 = reinterpret_cast<float*>(base + spec);

@@ -90,7 +90,8 @@ int gd_irfft2(void* spec, float* x, int N, int H, int W, void* stream);
  * conj(H) F(max(y,0)/alpha), F(u1), conj(H) F(v - u2) - since every step of the Gaussian iteration is
  * linear: one forward and one inverse transform per iteration.  GD_LLH_POISSON (sqrt in the V step)
  * keeps the OTF and u1, v - u2 as images.  Everything a later call needs is in `state`; `ws`
- * (gd_workspace_bytes) is scratch for the duration of one call only.
+ * (gd_workspace_bytes) is scratch for the duration of one call only.  The buffer's layout is private to
+ * the engine (at 256^2 the Gaussian slots are 256 KiB apart: HBM channel spread).
  *
  * gd_admm_init: OTF, x0 = clamp(init_l2) -> zin (the first denoiser input, x0 + u1 with u1 = 0),
  *               u1 = u2 = 0 and the first V step with rho2 = rho2_iters[..., 0].  llh = Gaussian: the

@@ -42,15 +42,27 @@ struct Bufs {
     Args a;
 };
 
-Bufs make(int N, float* par) {
+Bufs make(int N, float* par, bool placed = false) {
     const size_t img = (size_t)N * L * L, spec = (size_t)N * K * L;
     Bufs b;
-    CK(hipMalloc(&b.z, img * 4)); CK(hipMalloc(&b.zin, img * 4));
-    CK(hipMalloc(&b.state, 4 * spec * 8));
+    // placement experiment: KB_PAD bytes between the state slots, KB_ZPAD bytes in front of z and zin (multiples of 16)
+    // (the timing buffers only; the parity buffers keep the engine's contiguous slots)
+    const size_t pad = placed && getenv("KB_PAD") ? (size_t)atoll(getenv("KB_PAD")) / 16 * 2 : 0;    // in float2
+    const size_t zpad = placed && getenv("KB_ZPAD") ? (size_t)atoll(getenv("KB_ZPAD")) / 16 * 4 : 0; // in floats
+    // KB_LAYOUT=1: the engine's Gaussian layout (bind_state: |H|^2 takes half a slot); KB_ALIAS=1: z == zin (the
+    // identity denoiser's in-place iteration)
+    const bool eng = placed && getenv("KB_LAYOUT") && atoi(getenv("KB_LAYOUT")) == 1;
+    const bool alias = placed && getenv("KB_ALIAS") && atoi(getenv("KB_ALIAS")) == 1;
+    CK(hipMalloc(&b.z, (img + zpad) * 4)); CK(hipMalloc(&b.zin, (img + zpad) * 4));
+    CK(hipMalloc(&b.state, (4 * spec + 3 * pad) * 8));
     CK(hipMalloc(&b.ws, 2 * spec * 8));
     memset(&b.a, 0, sizeof(b.a));
     b.a.T = b.ws;
-    b.a.N = N; b.a.gH = b.a.gW = L; b.a.s_hh = (float*)b.state; b.a.s_g = b.state + spec; b.a.s_u1 = b.a.s_g + spec; b.a.s_w = b.a.s_u1 + spec;
+    b.a.N = N; b.a.gH = b.a.gW = L; b.a.s_hh = (float*)b.state;
+    b.a.s_g = b.state + (eng ? (spec + 1) / 2 : spec) + pad; b.a.s_u1 = b.a.s_g + spec + pad;
+    b.a.s_w = b.a.s_u1 + spec + pad;
+    b.z += zpad; b.zin += zpad;
+    if (alias) b.zin = b.z;
     b.a.a0 = b.z; b.a.o0 = b.zin;
     b.a.alpha = b.a.rho1 = b.a.rho2 = b.a.rho2n = GalScalar{par, 1};
     b.a.llh = GD_LLH_GAUSSIAN;
@@ -178,7 +190,7 @@ int main(int argc, char** argv) {
         printf("FAIL: k_gal_reg differs from the chained path\n");
         return 1;
     }
-    Bufs t = make(N, par);
+    Bufs t = make(N, par, true);
     seed(t, N);
     const double img_b = L * L * 4.0, half_b = K * L * 8.0;
     const double gb[4] = {N * (2 * img_b + 5.5 * half_b) / 1e9, N * (2 * img_b + 4.5 * half_b) / 1e9,
