@@ -654,13 +654,19 @@ def test_pipelined_chunks_bit_identical(dev):
 
 def _gauss_state_parts(st):
     """(|H|^2, G, W~) of an ADMMState's Gaussian state buffer (U1 excluded: the fused init parks the
-    PSF's row spectra and spilled registers there before iteration 0 writes it)."""
+    PSF's row spectra and spilled registers there before iteration 0 writes it).  Slots: |H|^2 (rounded up to
+    whole complex values), then G, U1, W~, with equal gaps between the slots (256 KiB at 256^2, else none:
+    gd_engine.hip kStateSlotGap) - the gap follows from gd_admm_state_bytes."""
     N, K, L = st.N, st.W // 2 + 1, st.H
     spec = N * K * L
+    hh_words = (spec + 1) // 2 * 2                 # floats
+    gap = (st.state.numel() - 4 * hh_words - 3 * 8 * spec) // 3 // 4   # floats
+    assert st.state.numel() == 4 * hh_words + 3 * 8 * spec + 3 * 4 * gap
     f = st.state.view(torch.float32)
     hh = f[:spec].view(N, K, L)
-    c = f[spec:].view(-1, 2)
-    return hh, c[:spec].reshape(N, K, L, 2), c[2 * spec:3 * spec].reshape(N, K, L, 2)
+    g0 = hh_words + gap
+    w0 = g0 + 2 * (2 * spec + gap)
+    return (hh, f[g0:g0 + 2 * spec].reshape(N, K, L, 2), f[w0:w0 + 2 * spec].reshape(N, K, L, 2))
 
 
 @pytest.mark.parametrize("N", [37, 300])
