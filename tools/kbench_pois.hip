@@ -29,7 +29,8 @@ int main(int argc, char** argv) {
     const size_t img = (size_t)N * L * L, spec = (size_t)N * K * L;
     float *z, *zin, *y, *w, *par; float2* st;
     CK(hipMalloc(&z, img * 4)); CK(hipMalloc(&zin, img * 4)); CK(hipMalloc(&y, img * 4)); CK(hipMalloc(&w, img * 4));
-    CK(hipMalloc(&st, 5 * spec * 8)); CK(hipMalloc(&par, N * 4));
+    const size_t pad = getenv("KB_PAD") ? (size_t)atoll(getenv("KB_PAD")) / 8 : 0;  // float2 between the state slots
+    CK(hipMalloc(&st, 5 * spec * 8 + 4 * pad * 8)); CK(hipMalloc(&par, N * 4));
     hipLaunchKernelGGL(k_fillp, dim3(4096), dim3(256), 0, 0, z, img, 1u, 0.f, 1.f);
     hipLaunchKernelGGL(k_fillp, dim3(4096), dim3(256), 0, 0, y, img, 2u, 10.f, 100.f);
     hipLaunchKernelGGL(k_fillp, dim3(4096), dim3(256), 0, 0, w, img, 3u, 0.f, 1.f);
@@ -43,8 +44,8 @@ int main(int argc, char** argv) {
 #endif
     Args a; memset(&a, 0, sizeof(a));
     a.N = N; a.llh = GD_LLH_POISSON;
-    a.s_hh = (float*)st; float2* c = st + spec / 2;
-    a.s_g = c; a.s_u1 = c + spec; a.s_w = c + 2 * spec; a.s_x = c + 3 * spec;
+    a.s_hh = (float*)st; float2* c = st + spec / 2 + pad;
+    a.s_g = c; a.s_u1 = c + spec + pad; a.s_w = c + 2 * (spec + pad); a.s_x = c + 3 * (spec + pad);
     a.a0 = z; a.o0 = zin; a.y = y; a.o1 = w;
     a.alpha = a.rho1 = a.rho2 = a.rho2n = GalScalar{par, 1};
     const double imgb = L * L * 4.0, halfb = K * L * 8.0;
