@@ -198,11 +198,14 @@ def graph_iter_ms(obs, psf, alpha, dev, reps=64, llh="Gaussian"):
         g.replay()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        g.replay()
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps
+        times = []
+        for _ in range(5):  # the median of 5 replays (one replay is ~0.4 ms: a single sample was noisy)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / reps)
+        return sorted(times)[len(times) // 2]
 
 
 def survey_bytes_per_galaxy(L, n, h=48):
@@ -640,7 +643,7 @@ def measure(args, ctx):
         # a short op of a host-bound eager forward (48^2): the events also time the host's enqueue gaps, so
         # the launch duration comes from back-to-back launches replayed as one hipGraph instead
         dom_ms = graph_iter_ms(obs, psf, alpha, dev, llh=args.llh)
-        timing = "64 back-to-back middle iterations (gd_admm_iter) replayed as one hipGraph, HIP events around it"
+        timing = "64 back-to-back middle iterations (gd_admm_iter) replayed as one hipGraph, HIP events around it, median of 5 replays"
     achieved = per_gal * N / (dom_ms * 1e-3) / 1e9 if per_gal else None
     traffic = None
     if args.traffic_json is None:
