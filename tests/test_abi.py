@@ -78,3 +78,9 @@ def test_argument_errors_need_no_device(lib):
     assert lib.gd_admm_state_bytes(3, 48, 48, 1) == 3 * 25 * 48 * 8 + 2 * 3 * 48 * 48 * 4
     # an odd number of |H|^2 values is padded to keep the complex arrays 8-byte aligned
     assert lib.gd_admm_state_bytes(1, 45, 45, 0) == (23 * 45 + 1) // 2 * 8 + 3 * 23 * 45 * 8
+    # at 256^2 the Gaussian slots are 256 KiB apart (HBM interleave spread, gd_engine.hip kStateSlotGap);
+    # the Poisson layout stays packed
+    spec = 3 * 129 * 256
+    assert lib.gd_admm_state_bytes(3, 256, 256, 0) == (spec + 1) // 2 * 8 + 3 * spec * 8 + 3 * 256 * 1024
+    assert lib.gd_admm_state_bytes(3, 256, 256, 1) == max(spec * 8 + 2 * 3 * 256 * 256 * 4,
+                                                          spec * 4 + 4 * spec * 8 + 3 * 256 * 256 * 4)
