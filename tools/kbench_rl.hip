@@ -28,9 +28,14 @@ int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 4096, n = argc > 2 ? atoi(argv[2]) : 100, reps = argc > 3 ? atoi(argv[3]) : 3;
     constexpr int L = 256, h = 48;
     float *y, *x, *psf; void *otf, *ws;
-    CK(hipMalloc(&y, (size_t)N * L * L * 4)); CK(hipMalloc(&x, (size_t)N * L * L * 4));
+    // placement experiment: KB_XPAD bytes in front of x (the output / iterate), KB_OPAD in front of the OTF
+    const size_t xpad = getenv("KB_XPAD") ? (size_t)atoll(getenv("KB_XPAD")) / 4 : 0;
+    const size_t opad = getenv("KB_OPAD") ? (size_t)atoll(getenv("KB_OPAD")) : 0;
+    CK(hipMalloc(&y, (size_t)N * L * L * 4)); CK(hipMalloc(&x, ((size_t)N * L * L + xpad) * 4));
+    x += xpad;
     CK(hipMalloc(&psf, (size_t)N * h * h * 4));
-    CK(hipMalloc(&otf, gd_otf_bytes(N, L, L))); CK(hipMalloc(&ws, gd_workspace_bytes(N, L, L)));
+    CK(hipMalloc(&otf, gd_otf_bytes(N, L, L) + opad)); CK(hipMalloc(&ws, gd_workspace_bytes(N, L, L)));
+    otf = (char*)otf + opad;
     hipLaunchKernelGGL(k_img, dim3(4096), dim3(256), 0, 0, y, (size_t)N * L * L, 1u);
     hipLaunchKernelGGL(k_psf, dim3(N), dim3(256), 0, 0, psf, N, h);
     if (gd_psf_to_otf(psf, h * h, h, h, N, L, L, otf, ws, nullptr) != GD_OK) { printf("otf: %s\n", gd_last_error()); return 1; }
