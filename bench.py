@@ -240,6 +240,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--blocks", type=int, default=3, help="timed blocks of --steps steps (value = the median block)")
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=4096, help="galaxies per GPU")
     p.add_argument("--size", type=int, default=256)
@@ -479,35 +480,58 @@ def measure(args, ctx):
                 torch.cuda.synchronize()
         torch.cuda.synchronize()
         settle_s = time.perf_counter() - ts
-        if world > 1:
-            dist.barrier()
-        # the timed region: no profiling events (value is the clean rate)
-        _lib.profile_enable(0)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if world > 1:
-            dist.barrier()
-        assert torch.isfinite(out).all(), "non-finite output"
-        # a separate pass of the same K steps with the library's HIP events on (per operation on the
-        # caller's stream; per launch too when nothing is pipelined): the roofline's launch durations
-        _lib.profile_reset()
-        _lib.profile_enable(1 if chunk_bytes > 0 else 2)
-        torch.cuda.synchronize()
-        tp = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        tp = time.perf_counter() - tp
-        _lib.profile_enable(0)
-        kstats = _lib.profile_collect()
+        # the hipGraph of the same forward (gdeconv.graphs), captured before the timed blocks so that its replayed
+        # blocks interleave with the eager ones in one clock window: what a serving loop pays once host launch
+        # overhead is gone (matters at 48^2; reported beside value, not as value)
+        gf = None
+        if not args.no_graph:
+            progress("hipGraph capture")
+            from gdeconv.graphs import GraphedForward
+            gf = GraphedForward(model, obs, psf, alpha)
+            gout = gf.replay()
+            torch.cuda.synchronize()
 
-    progress(f"timed region {(t1 - t0) * 1e3:.1f} ms for {args.steps} steps; profiling pass {tp * 1e3:.1f} ms")
-    rank_times = all_ranks(t1 - t0, world, backend, dev)
-    elapsed = max(rank_times)
+        def timed(fn, prof=0):
+            """K steps of fn bracketed by a barrier + synchronize on both sides; max over ranks (seconds)."""
+            if world > 1:
+                dist.barrier()
+            if prof:
+                _lib.profile_enable(prof)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(args.steps):
+                r = fn()
+            torch.cuda.synchronize()
+            t = time.perf_counter() - t
+            if prof:
+                _lib.profile_enable(0)
+            return max_over_ranks(t, world, backend, dev), r
+
+        # B timed blocks of exactly K steps each; after every eager block (no profiling events: value's blocks) the
+        # same window runs K replayed steps (if graphed) and K steps with the library's HIP events on (per operation
+        # on the caller's stream, per launch too when nothing is pipelined: the roofline's launch durations).
+        # value = the MEDIAN eager block; every block is recorded.
+        _lib.profile_enable(0)
+        _lib.profile_reset()
+        prof_level = 1 if chunk_bytes > 0 else 2
+        te_blocks, tg_blocks, tp_blocks, rank_blocks = [], [], [], []
+        for _ in range(args.blocks):
+            t_, out = timed(step)
+            te_blocks.append(t_)
+            rank_blocks.append(all_ranks(t_, world, backend, dev) if world > 1 else [t_])
+            if gf is not None:
+                t_, gout = timed(gf.replay)
+                tg_blocks.append(t_)
+            tp_blocks.append(timed(step, prof_level)[0])
+        kstats = _lib.profile_collect()
+        assert torch.isfinite(out).all(), "non-finite output"
+
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+    elapsed = med(te_blocks)
+    tp = med(tp_blocks)
+    progress(f"eager blocks {[round(t * 1e3 / args.steps, 3) for t in te_blocks]} ms/step; replayed "
+             f"{[round(t * 1e3 / args.steps, 3) for t in tg_blocks]}; profiled {[round(t * 1e3 / args.steps, 3) for t in tp_blocks]}")
+    rank_times = rank_blocks[te_blocks.index(elapsed)]
     gal_s = N * world * args.steps / elapsed
 
     gather_ms, with_gather = None, None
@@ -539,40 +563,11 @@ def measure(args, ctx):
                        "ms_per_step": tw * 1e3 / args.steps,
                        "note": "each step's outputs all-gathered to every rank, overlapped with the next step"}
 
-    # the same forward captured once as a hipGraph (gdeconv.graphs) and replayed: what a serving loop
-    # pays once host launch overhead is gone (matters at 48^2; reported beside value, not as value)
     graphed = None
-    if not args.no_graph:
-        progress("hipGraph capture and interleaved eager / replayed blocks")
-        from gdeconv.graphs import GraphedForward
-        gf = GraphedForward(model, obs, psf, alpha)
-        gout = gf.replay()
-        torch.cuda.synchronize()
-
-        def timed(fn):
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            for _ in range(args.steps):
-                r = fn()
-            torch.cuda.synchronize()
-            return max_over_ranks(time.perf_counter() - t, world, backend, dev), r
-
-        # eager and replayed blocks interleaved (3 rounds, medians): the same clock window for both, so
-        # the comparison is not a property of which ran first on a warming / throttling chip
-        teg, tgs = [], []
-        with torch.no_grad():
-            for _ in range(3):
-                teg.append(timed(step)[0])
-                tg_, gout = timed(gf.replay)
-                tgs.append(tg_)
-        tgr, teag = sorted(tgs)[1], sorted(teg)[1]
+    if gf is not None:
+        tgr = med(tg_blocks)
         graphed = {"value": N * world * args.steps / tgr, "unit": "galaxies/s", "ms_per_step": tgr * 1e3 / args.steps,
-                   "eager_interleaved": {"value": N * world * args.steps / teag, "ms_per_step": teag * 1e3 / args.steps},
-                   "blocks_ms_per_step": {"eager": [round(t * 1e3 / args.steps, 4) for t in teg],
-                                          "graphed": [round(t * 1e3 / args.steps, 4) for t in tgs]},
-                   "note": "medians of 3 interleaved blocks of K eager / K replayed steps (no per-op profiling events)",
+                   "note": "median of the replayed blocks interleaved with value's eager blocks (no per-op profiling events)",
                    "bit_identical_to_eager": bool(torch.equal(gout, out))}
         del gf, gout
 
@@ -638,7 +633,7 @@ def measure(args, ctx):
         dom_raw = max(priced, key=lambda k: kern[k][0])
         dom_ms = kern[dom_raw][0] / kern[dom_raw][1]
         per_gal = kernel_bytes(dom_raw, L, n)
-    timing = "HIP events on the caller's stream around each call, profiling pass"
+    timing = "HIP events on the caller's stream around each call, the profiled blocks interleaved with value's blocks"
     if (not rl and dom_ms < 0.05 and pretty(dom_raw) == f"op_admm_iter<{L},{args.llh}>"):
         # a short op of a host-bound eager forward (48^2): the events also time the host's enqueue gaps, so
         # the launch duration comes from back-to-back launches replayed as one hipGraph instead
@@ -727,9 +722,14 @@ def measure(args, ctx):
                                        "not this engine's traffic (see roofline / kernels.*.algorithmic_bytes_per_call)"},
         "kernels": kernels,
     }
-    rec["profiling_pass"] = {"ms_per_step": tp * 1e3 / args.steps,
-                             "note": "kernels.* and roofline come from a second pass of the same K steps with the "
-                                     "library's HIP events on; value is the event-free timed region"}
+    rec["blocks"] = {"eager_ms_per_step": [round(t * 1e3 / args.steps, 4) for t in te_blocks],
+                     "graphed_ms_per_step": [round(t * 1e3 / args.steps, 4) for t in tg_blocks],
+                     "profiled_ms_per_step": [round(t * 1e3 / args.steps, 4) for t in tp_blocks],
+                     "eager_spread": max(te_blocks) / min(te_blocks) - 1.0,
+                     "value_vs_profiled": gal_s / (N * world * args.steps / tp) - 1.0,
+                     "note": f"{args.blocks} rounds of [K eager steps, K replayed steps, K profiled steps] after the "
+                             "warmup and clock settling; value and ms_per_step = the median eager block; kernels.* and "
+                             "roofline = the HIP events of the profiled blocks of the same window"}
     if world > 1:
         rec["ranks"] = {"elapsed_s_min": min(rank_times), "elapsed_s_max": max(rank_times),
                         "spread": max(rank_times) / min(rank_times) - 1.0, "per_rank_galaxies": N}
@@ -743,8 +743,6 @@ def measure(args, ctx):
         rec["with_gather"] = with_gather
     if graphed is not None:
         rec["graphed"] = graphed
-        # value (the first timed block) against the same run's later interleaved eager blocks
-        rec["value_vs_interleaved_eager"] = gal_s / graphed["eager_interleaved"]["value"] - 1.0
     if ingest is not None:
         rec["ingest"] = ingest
 

@@ -403,47 +403,16 @@ struct ColTraits {
 #ifndef GD_RCP_DIV
 #define GD_RCP_DIV 1  // Gaussian spectral update: reciprocal-multiply instead of division (-5 % iteration time)
 #endif
-// Streaming (single-use per iteration) state traffic marked non-temporal.  Measured on op_admm_iter:
-// stores (U1, W~, zin) 1.673/1.692 -> 1.658/1.666 ms - on; loads (z, |H|^2, G, U1, W~) 1.75-1.87 ms,
-// i.e. slower - off.  The parked registers stay ordinary (they are re-read by the same CU).
-#ifndef GD_NT_LD
-#define GD_NT_LD 0
-#endif
-#ifndef GD_NT_ST
-#define GD_NT_ST 1
-#endif
-__device__ __forceinline__ float ld_s(const float* p) {
-#if GD_NT_LD
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ float2 ld_s(const float2* p) {
-#if GD_NT_LD
-    const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p));
-    float2 r;
-    __builtin_memcpy(&r, &v, 8);
-    return r;
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ void st_s(float* p, float v) {
-#if GD_NT_ST
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+// Streaming (single-use per iteration) state traffic: stores non-temporal, loads ordinary.  Measured on
+// op_admm_iter (round 1): non-temporal stores (U1, W~, zin) 1.673/1.692 -> 1.658/1.666 ms; non-temporal loads
+// (z, |H|^2, G, U1, W~) 1.75-1.87 ms, i.e. slower.  The parked registers stay ordinary (re-read by the same CU).
+__device__ __forceinline__ float ld_s(const float* p) { return *p; }
+__device__ __forceinline__ float2 ld_s(const float2* p) { return *p; }
+__device__ __forceinline__ void st_s(float* p, float v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void st_s(float2* p, float2 v) {
-#if GD_NT_ST
     unsigned long long u;
     __builtin_memcpy(&u, &v, 8);
     __builtin_nontemporal_store(u, reinterpret_cast<unsigned long long*>(p));
-#else
-    *p = v;
-#endif
 }
 // Gaussian ADMM state layout (|H|^2, G, U1, W~; [N][K][L], one column of L bins per (galaxy, kx)).  At
 // L = 256 the bins inside a column are stored in the order the fused iteration's column lines hold
@@ -2353,31 +2322,61 @@ int g_subnet_fused_max = 256;
 int g_sri_map = 0;  // k_subnet_rhos_init's block -> (role, galaxy) map (tools/kbench_small)
 int g_fused_init = 1;  // Gaussian init (256^2: k_psf_rows<STATE> + k_gal_reg_init) and the other one-launch inits: 1 on; 0 = chunked
 
-// Under stream capture a pipelined operation takes its fork / join events from a ring of kCapSets sets, so no event
-// is recorded twice inside one captured forward (GD_CAPTURE_PIPELINE, below).
+// Eager pipelined operations fork onto the device's internal streams (PipeRes, shared by the host threads, one
+// operation at a time under its mutex).  Under stream capture (mode 2, gd_set_capture_pipeline) an operation
+// forks onto streams of the CALLING HOST THREAD instead (CapRes): those streams join the capture and stay in it
+// until hipStreamEndCapture, so they must never be the streams another thread's eager calls enqueue on.  Each
+// captured operation takes its fork / join events from a ring of kCapSets sets, so no event is recorded twice
+// inside one captured forward.
 constexpr int kCapSets = 64;
 struct PipeRes {
     bool ok = false;
     hipStream_t st[kMaxPipe];
     hipEvent_t fork;
     hipEvent_t join[kMaxPipe];
-    hipEvent_t cfork[kCapSets];
-    hipEvent_t cjoin[kCapSets][kMaxPipe];
-    int cpos = 0;
     // held from the fork record to the last join wait of one pipelined call: the fork / join events and
     // the internal streams are per device, so concurrent callers (host threads) enqueue one at a time
     std::mutex mu;
 };
 PipeRes g_pipe[64];
 std::mutex g_pipe_mu;
+struct CapRes {
+    hipStream_t st[kMaxPipe];
+    hipEvent_t cfork[kCapSets];
+    hipEvent_t cjoin[kCapSets][kMaxPipe];
+    int cpos = 0;
+};
+// per host thread and device, created at the thread's first pipelined capture; never freed (a thread's streams and
+// events outlive it: destroying them from a thread-exit handler can race the runtime's own teardown)
+thread_local CapRes* t_cap[64];
 
 thread_local int g_capture_pipe_override = -1;  // gd_set_capture_pipeline (per host thread)
 inline int capture_pipeline_mode() {
+    // default 0 (chunks in sequence on the capturing stream): a fork from a stream that itself joined the capture
+    // through an event onto internal streams crashed the ROCm 7 runtime inside hipStreamEndCapture;
+    // callers that fork from the capturing stream itself (gdeconv.graphs.GraphedForward) opt in to 2
     static const int mode = [] {
         const char* e = std::getenv("GD_CAPTURE_PIPELINE");
-        return e ? std::atoi(e) : 2;
+        const int m = e ? std::atoi(e) : 0;
+        return m == 2 ? 2 : 0;
     }();
     return g_capture_pipe_override >= 0 ? g_capture_pipe_override : mode;
+}
+
+inline CapRes* cap_res() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (t_cap[dev]) return t_cap[dev];
+    CapRes* r = new CapRes();
+    for (int i = 0; i < kMaxPipe; ++i)
+        if (hipStreamCreateWithFlags(&r->st[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (int c = 0; c < kCapSets; ++c) {
+        if (hipEventCreateWithFlags(&r->cfork[c], hipEventDisableTiming) != hipSuccess) return nullptr;
+        for (int i = 0; i < kMaxPipe; ++i)
+            if (hipEventCreateWithFlags(&r->cjoin[c][i], hipEventDisableTiming) != hipSuccess) return nullptr;
+    }
+    t_cap[dev] = r;
+    return r;
 }
 
 inline PipeRes* pipe_res() {
@@ -2391,11 +2390,6 @@ inline PipeRes* pipe_res() {
             if (hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming) != hipSuccess) return nullptr;
         }
         if (hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-        for (int c = 0; c < kCapSets; ++c) {
-            if (hipEventCreateWithFlags(&r.cfork[c], hipEventDisableTiming) != hipSuccess) return nullptr;
-            for (int i = 0; i < kMaxPipe; ++i)
-                if (hipEventCreateWithFlags(&r.cjoin[c][i], hipEventDisableTiming) != hipSuccess) return nullptr;
-        }
         r.ok = true;
     }
     return &r;
@@ -2442,50 +2436,50 @@ int for_chunks_hw(const Args& a, int H, int W, hipStream_t st, F&& f) {
     if (G >= a.N) return f(a, st);
     int S = g_pipe_streams < kMaxPipe ? g_pipe_streams : kMaxPipe;
     if (S > a.N / G) S = a.N / G;  // regions must fit the caller's workspace
-    // Under stream capture (GD_CAPTURE_PIPELINE, or gd_set_capture_pipeline per host thread): 0 = the chunks in
-    // sequence on the caller's stream; 1 = pipelined with the shared fork / join events; 2 = pipelined, each
-    // operation's fork / join on its own event set from the ring (default).  Round 5 (profiles/r05_capture_*):
-    // the round-4 crash inside hipStreamEndCapture (4096 x 160^2, profiles/r04dbg_160_graph_crash.txt) is not the
-    // event re-use - mode 2 crashes the same way - but a fork from a stream that itself joined the capture through
-    // an event (ADMMState.init_concurrent's side stream) onto these internal streams, inside torch's capture:
-    // forked from the capturing stream itself, mode 2 captures, instantiates and replays bit-identically.  The
-    // same fork / join in plain HIP (tools/capture_probe.hip: shared or fresh events, nested, streams created
-    // during the capture, temporary events destroyed) does not crash.  So the engine runs a side-stream init with
-    // mode 0 under capture (gdeconv/engine.py) and everything else with mode 2.
+    // Under stream capture (GD_CAPTURE_PIPELINE, or gd_set_capture_pipeline per host thread): 0 (default) = the
+    // chunks in sequence on the capturing stream; 2 = pipelined over the calling thread's capture streams, each
+    // operation's fork / join on its own event set from the ring.  Round 5 (profiles/r05_capture_*): the round-4 crash
+    // inside hipStreamEndCapture (4096 x 160^2, profiles/r04dbg_160_graph_crash.txt) came with a fork from a stream
+    // that itself joined the capture through an event (ADMMState.init_concurrent's side stream) onto internal streams;
+    // forked from the capturing stream itself, mode 2 captures, instantiates and replays bit-identically.  The same
+    // fork / join in plain HIP (tools/capture_probe.hip) does not crash.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     const bool capturing = S > 1 && hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
-    const int cmode = capture_pipeline_mode();
-    if (capturing && cmode == 0) S = 1;
-    PipeRes* r = S > 1 ? pipe_res() : nullptr;
-    if (!r) S = 1;
+    if (capturing && capture_pipeline_mode() != 2) S = 1;
+    PipeRes* r = (S > 1 && !capturing) ? pipe_res() : nullptr;
+    CapRes* cr = (S > 1 && capturing) ? cap_res() : nullptr;
+    if (!r && !cr) S = 1;
     std::unique_lock<std::mutex> lk;
-    if (S > 1) lk = std::unique_lock<std::mutex>(r->mu);
+    if (r) lk = std::unique_lock<std::mutex>(r->mu);
     hipEvent_t fork = nullptr;
     hipEvent_t* join = nullptr;
+    hipStream_t* streams = nullptr;
     if (S > 1) {
-        if (capturing && cmode == 2) {
-            const int c = r->cpos;
-            r->cpos = (c + 1) % kCapSets;
-            fork = r->cfork[c];
-            join = r->cjoin[c];
+        if (cr) {
+            const int c = cr->cpos;
+            cr->cpos = (c + 1) % kCapSets;
+            fork = cr->cfork[c];
+            join = cr->cjoin[c];
+            streams = cr->st;
         } else {
             fork = r->fork;
             join = r->join;
+            streams = r->st;
         }
         if (hipEventRecord(fork, st) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
         for (int i = 0; i < S; ++i)
-            if (hipStreamWaitEvent(r->st[i], fork, 0) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
+            if (hipStreamWaitEvent(streams[i], fork, 0) != hipSuccess) return fail(GD_ERR_HIP, "pipeline fork");
     }
     int rc = GD_OK;
     for (int g0 = 0, c = 0; g0 < a.N && rc == GD_OK; g0 += G, ++c) {
         const int n = (a.N - g0 < G) ? a.N - g0 : G;
         Args b = offset_args(a, g0, n, H, W);
         b.T = a.T + (size_t)(c % S) * G * 2 * (W / 2 + 1) * H;
-        rc = f(b, S > 1 ? r->st[c % S] : st);
+        rc = f(b, S > 1 ? streams[c % S] : st);
     }
     if (S > 1) {
         for (int i = 0; i < S; ++i) {
-            if (hipEventRecord(join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(st, join[i], 0) != hipSuccess)
+            if (hipEventRecord(join[i], streams[i]) != hipSuccess || hipStreamWaitEvent(st, join[i], 0) != hipSuccess)
                 return fail(GD_ERR_HIP, "pipeline join");
         }
     }
@@ -2848,7 +2842,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r05.5"; }
+const char* gd_engine_rev(void) { return "r06.0"; }
 
 // the source hash __graft_entry__.build() computed (gdeconv._lib.source_hash); the "gdsrc:" marker lets the
 // build find it in the binary without loading it
@@ -3232,8 +3226,10 @@ size_t gd_set_chunk_bytes(size_t bytes) {
 }
 
 int gd_set_capture_pipeline(int mode) {
+    // (GD_ERR_ARG is -1, the "no override" value: an invalid mode answers GD_ERR_UNSUPPORTED)
+    if (mode != -1 && mode != 0 && mode != 2) return fail(GD_ERR_UNSUPPORTED, "capture pipeline mode must be -1, 0 or 2");
     const int old = g_capture_pipe_override;
-    g_capture_pipe_override = (mode >= 0 && mode <= 2) ? mode : -1;
+    g_capture_pipe_override = mode;
     return old;
 }
 
@@ -3244,14 +3240,16 @@ int gd_set_pipeline_streams(int streams) {
 }
 
 int gd_set_fused_init(int on) {
+    if (on != 0 && on != 1) return fail(GD_ERR_ARG, "gd_set_fused_init: 0 or 1");
     const int old = g_fused_init;
-    g_fused_init = on ? 1 : 0;
+    g_fused_init = on;
     return old;
 }
 
 int gd_set_fused_rl(int on) {
+    if (on != 0 && on != 1) return fail(GD_ERR_ARG, "gd_set_fused_rl: 0 or 1");
     const int old = g_fused_rl;
-    g_fused_rl = on ? 1 : 0;
+    g_fused_rl = on;
     return old;
 }
 
@@ -3262,8 +3260,9 @@ int gd_set_subnet_fused_max(int n) {
 }
 
 int gd_set_fused_iteration(int on) {
+    if (on != 0 && on != 1) return fail(GD_ERR_ARG, "gd_set_fused_iteration: 0 or 1");
     const int old = g_fused;
-    g_fused = on ? 1 : 0;
+    g_fused = on;
     return old;
 }
 

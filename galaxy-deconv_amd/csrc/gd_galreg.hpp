@@ -35,29 +35,6 @@ __device__ __forceinline__ void pin(float2 (&v)[N]) {
     for (int i = 0; i < N; i += 4) pin4(v[i], v[i + 1], v[i + 2], v[i + 3]);
 }
 
-// ---- Cache warming for the galaxy that will run next on this XCD.  Workgroups go to the XCDs round-robin
-// (block b -> XCD b mod 8 in practice; used for speed only), so galaxy g + 256 runs on g's XCD.  Phase I
-// of galaxy g issues LDS-DMA loads of that galaxy's rows (global_load_lds_dwordx4: 16 bytes per lane,
-// written into a 1 KiB sink nobody reads, no registers held), so its R phase finds them in the L2 /
-// Infinity Cache instead of waiting on HBM.  Ends with s_waitcnt vmcnt(0) before the workgroup exits.
-// Measured (profiles/r02m_warm.txt): the R phase's z wait 9.9 -> 5.7 us, but phase I grows 2 x 4.6 us
-// (the DMA issue and its traffic beside the zin stores): MID 1.642 -> 1.707 ms, init 1.41 -> 1.47 ms.
-// Off; kept as an experiment switch.
-#ifndef GD_REG_PF
-#define GD_REG_PF 0
-#endif
-typedef __attribute__((address_space(3))) void* lds_vptr;
-typedef __attribute__((address_space(1))) void* gbl_vptr;
-template <int L, int PART, int NPART>
-__device__ __forceinline__ void warm_next(const float* base, int g, int N, float4* sink, int tid, int nthreads) {
-    if (!GD_REG_PF) return;
-    const int gn = g + 256;
-    if (gn >= N) return;
-    const float4* src = reinterpret_cast<const float4*>(base + (size_t)gn * L * L);
-    constexpr int V4 = L * L / 4, PER = V4 / NPART;
-    for (int i = PART * PER + tid; i < (PART + 1) * PER; i += nthreads)
-        __builtin_amdgcn_global_load_lds((gbl_vptr)(src + i), (lds_vptr)sink, 16, 0, 0);
-}
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---- 16-byte state access.  At 256^2 the Gaussian state's bins inside a column are stored in the
@@ -68,72 +45,9 @@ __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" :
 __device__ __forceinline__ int soff_c(int kx, int m, int j) { return kx * 256 + 32 * m + 2 * j; }  // bins j + 16 (2m + e)
 __device__ __forceinline__ int soff_h(int kx, int q, int j) { return kx * 256 + 64 * q + 4 * j; }  // bins j + 16 (4q + e)
 __device__ __forceinline__ f4v ld4v(const void* p) { return *reinterpret_cast<const f4v*>(p); }
-#ifndef GD_REG_NTL
-#define GD_REG_NTL 0  // 1: the iteration's state loads non-temporal
-#endif
-__device__ __forceinline__ f4v ld4s(const void* p) {
-#if GD_REG_NTL
-    return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-#else
-    return *reinterpret_cast<const f4v*>(p);
-#endif
-}
-__device__ __forceinline__ void st4v(void* p, f4v v) {
-#if GD_NT_ST
-    __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
-#else
-    *reinterpret_cast<f4v*>(p) = v;
-#endif
-}
-
-// ---- 16-byte image accesses staged through the line's LDS exchange area (GD_REG_Z16).  The line FFTs want lane j
-// of a line to hold x[j + 16 r] of the pair's two rows (4-byte accesses: 64 B per line and wave instruction, each
-// 128-B line touched by two instructions).  Instead a lane loads (stores) 16 B at columns 4 j + 64 c, c < 4, of each
-// row - 256 contiguous bytes per line and instruction, a quarter of the instructions - and the values move to (from)
-// the FFT layout through the line's exchange area (272 float2 >= the pair's 256 columns, (row 2p, row 2p + 1)
-// interleaved per column: two ds_write_b128 per float4 pair, ds_read_b64 per register).  The kbench_stream pattern
-// test put the 4-byte form at 5.42 TB/s and the 16-byte one at 5.81 TB/s for k_gal_reg's own bytes and order
-// (profiles/r05b_kstream.txt).
-#ifndef GD_REG_Z16
-#define GD_REG_Z16 0  // bit 0: z loads, bit 1: zin stores (measured: +0.5 ... +2 %, off)
-#endif
-// the pair's 8 float4 (row 2p at c < 4, row 2p + 1 at 4 + c); r0 = row 2p + 4 j
-__device__ __forceinline__ void z16_load(f4v (&Z)[8], const float* r0, int L) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        Z[c] = ld4v(r0 + 64 * c);
-        Z[4 + c] = ld4v(r0 + L + 64 * c);
-    }
-}
-// Z -> X[r] = (x_2p[j + 16 r], x_2p+1[j + 16 r]) through xs (the line's exchange area); MAP(a, b) is applied to
-// each value first (e.g. max(y, 0) / alpha)
-template <typename F>
-__device__ __forceinline__ void z16_unpack(float2 (&X)[16], const f4v (&Z)[8], float2* xs, int j, F&& map) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const f4v a = Z[c], b = Z[4 + c];
-        *reinterpret_cast<f4v*>(xs + 4 * j + 64 * c) = f4v{map(a[0]), map(b[0]), map(a[1]), map(b[1])};
-        *reinterpret_cast<f4v*>(xs + 4 * j + 64 * c + 2) = f4v{map(a[2]), map(b[2]), map(a[3]), map(b[3])};
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) X[r] = xs[j + 16 * r];
-    wave_lds_sync();  // the reads complete before the line's FFT rewrites the area
-}
-// V[r] = (row 2p, row 2p + 1) at columns j + 16 r -> 16-byte non-temporal stores of both rows; o = row 2p
-__device__ __forceinline__ void z16_store(float* o, const float2 (&V)[16], float2* xs, int j, int L) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) xs[j + 16 * r] = V[r];
-    wave_lds_sync();
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const f4v a = *reinterpret_cast<const f4v*>(xs + 4 * j + 64 * c);
-        const f4v b = *reinterpret_cast<const f4v*>(xs + 4 * j + 64 * c + 2);
-        st4v(o + 4 * j + 64 * c, f4v{a[0], a[2], b[0], b[2]});
-        st4v(o + L + 4 * j + 64 * c, f4v{a[1], a[3], b[1], b[3]});
-    }
-    wave_lds_sync();
-}
+__device__ __forceinline__ f4v ld4s(const void* p) { return *reinterpret_cast<const f4v*>(p); }
+// state / image stores are single-use per iteration: non-temporal (st_s, gd_engine.hip)
+__device__ __forceinline__ void st4v(void* p, f4v v) { __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p)); }
 
 // Poisson pass A's bin (the X update and u1's dual, models/Unrolled_ADMM.py:209, :212, on spectra).  The
 // state holds H (the OTF, G slot) and W = F(w), w = v - u2 (written by pass B, unmultiplied), so pass A
@@ -288,41 +202,19 @@ __device__ __forceinline__ void fused_update4x(const Args& a, float2 (&C)[NC][16
     }
 }
 
-// experiment switch: GD_REG_NOFFT = 1 skips every transform (memory and LDS skeleton only)
-// register-allocation switches: materialise the column transforms' outputs where they are computed
-#ifndef GD_REG_PINF
-#define GD_REG_PINF 0
-#endif
-#ifndef GD_REG_PINI
-#define GD_REG_PINI 0
-#endif
-#ifndef GD_REG_NOFFT
-#define GD_REG_NOFFT 0
-#endif
 #ifndef GD_REG_LEAN
 #define GD_REG_LEAN 1  // 1: twiddles W^{j k1} synthesised from 6 table entries; 0: 15 table reads
 #endif
 template <int L, bool INV, bool DPP = false>
 __device__ __forceinline__ void reg_fft(float2 (&v)[16], int j, float2* xch, const float2* tw) {
-#if GD_REG_NOFFT
-    asm volatile("" ::: "memory");
-#else
     line_fft<L, INV, GD_REG_LEAN != 0, DPP>(v, j, xch, tw);
-#endif
 }
 // two independent lines' transforms interleaved through one exchange area (line_fft2; bit-identical to two reg_fft)
 template <int L, bool INV>
 __device__ __forceinline__ void reg_fft2(float2 (&v0)[16], float2 (&v1)[16], int j, float2* xch, const float2* tw) {
-#if GD_REG_NOFFT
-    asm volatile("" ::: "memory");
-#else
     line_fft2<L, INV, GD_REG_LEAN != 0>(v0, v1, j, xch, tw);
-#endif
 }
 
-#ifndef GD_REG_SLD_PAD
-#define GD_REG_SLD_PAD 1
-#endif
 template <int L>
 struct RegGeo {
     static constexpr int F1 = Plan<L>::F1, F2 = Plan<L>::F2, K = L / 2 + 1;
@@ -332,7 +224,7 @@ struct RegGeo {
     // slice layout [pair][SLD] (k_gal_iter's, one slot longer): an odd row stride puts the 16 rows a
     // line writes in phase I (column results -> row half spectra) on 16 distinct bank pairs (SLD = 132
     // put every fourth row on the same banks: 4-way conflicts on those stores)
-    static constexpr int SLD = FusedGeo<L>::SLD + GD_REG_SLD_PAD;
+    static constexpr int SLD = FusedGeo<L>::SLD + 1;
     static constexpr int XCH = xch_elems<L>();
     static constexpr int HPL = (NP / 2) / LINES;                // row pairs per line in a half of phase I
     static constexpr int U = cmax(NP * SLD, LINES * XCH);
@@ -368,9 +260,11 @@ struct RegGeo {
 #ifndef GD_STAGGER_N
 #define GD_STAGGER_N 4  // groups of the first round (group k starts k / N of the spread late)
 #endif
+// Only when the launch spans more than one round of workgroups (N > 256 galaxies at one per CU): a single round has
+// no later rounds to phase-lock, and its staggered groups would only start late.
 template <int US>
-__device__ __forceinline__ void stagger_start(int g) {
-    if (US > 0 && g < 256 && (g % GD_STAGGER_N) != 0) {
+__device__ __forceinline__ void stagger_start(int g, int N) {
+    if (US > 0 && N > 256 && g < 256 && (g % GD_STAGGER_N) != 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long d = (unsigned long long)US * 100 * (g % GD_STAGGER_N) / GD_STAGGER_N;
         while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(32);
@@ -393,7 +287,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
     __shared__ float2 nyqx[L];      // line 0's split scratch (S is occupied)
     __shared__ float nyqo[L];       // x(., L/2)
-    __shared__ float4 pf_sink[64];  // warm_next's LDS-DMA target (never read)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int b = blockIdx.x, g = a.rev ? a.N - 1 - b : b;
     const bool l0 = (line == 0);
@@ -407,15 +300,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 
     // R
     float2 X[RG::PPL][F2];
-#if GD_REG_Z16 & 1
-    f4v Z4[RG::PPL][8];
-    {
-        const float* z = a.a0 + (size_t)g * L * L;
-#pragma unroll
-        for (int q = 0; q < RG::PPL; ++q)
-            z16_load(Z4[q], z + (size_t)(2 * (opaque(line) + LINES * q)) * L + 4 * opaque(j), L);
-    }
-#else
     {
         const float* z = a.a0 + (size_t)g * L * L;
 #pragma unroll
@@ -426,15 +310,11 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(ld_s(r0 + F1 * r), ld_s(r0 + L + F1 * r));
         }
     }
-#endif
-    stagger_start<GD_REG_STAGGER>(b);  // (z's loads are in flight meanwhile)
+    stagger_start<GD_REG_STAGGER>(b, a.N);  // (z's loads are in flight meanwhile)
     __syncthreads();  // twiddles
     GD_TRACE(1);
 #pragma unroll
     for (int q = 0; q < RG::PPL; ++q) {
-#if GD_REG_Z16 & 1
-        z16_unpack(X[q], Z4[q], my, opaque(j), [](float v) { return v; });
-#endif
         reg_fft<L, false>(X[q], opaque(j), my, tw);
         pin(X[q]);
         __builtin_amdgcn_sched_barrier(0);
@@ -487,7 +367,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false>(CA[u], opaque(j), my, tw);
-            if (GD_REG_PINF) pin(CA[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -522,7 +401,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CA[u], opaque(j), my, tw);
-        if (GD_REG_PINI || POIS) pin(CA[u]);  // Poisson pass A: spill-free with the inverses pinned
+        if (POIS) pin(CA[u]);  // Poisson pass A: spill-free with the inverses pinned
         __builtin_amdgcn_sched_barrier(0);
     }
     if (l0) {
@@ -570,7 +449,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int u = 0; u < RG::CPL; ++u) {
             reg_fft<L, false>(CB[u], opaque(j), my, tw);
-            if (GD_REG_PINF) pin(CB[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -582,7 +460,7 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
     for (int u = 0; u < RG::CPL; ++u) {
         reg_fft<L, true>(CB[u], opaque(j), my, tw);
-        if (GD_REG_PINI || POIS) pin(CB[u]);
+        if (POIS) pin(CB[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -606,7 +484,6 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
             }
         }
         for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        warm_next<L, hf, 2>(a.a0, g, a.N, pf_sink, tid, T);
         lds_barrier();
         float2 V[RG::HPL][F2];
 #pragma unroll
@@ -632,28 +509,22 @@ __global__ __launch_bounds__(512) void k_gal_reg(Args a) {
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
             reg_fft<L, true>(V[w], opaque(j), my, tw);
-#if !(GD_REG_Z16 & 2)
             // (the row pointer ahead of Poisson's scaling: formed after it, pass A spilled 4 VGPRs)
             float* o = out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L + opaque(j);
-#endif
             if constexpr (POIS) {
                 if (last) {  // x * alpha for Poisson (:215)
 #pragma unroll
                     for (int r = 0; r < F2; ++r) V[w][r] = make_float2(V[w][r].x * al, V[w][r].y * al);
                 }
             }
-#if GD_REG_Z16 & 2
-            z16_store(out + (size_t)(hf * L / 2 + 2 * (opaque(line) + LINES * w)) * L, V[w], my, opaque(j), L);
-#else
 #pragma unroll
             for (int r = 0; r < F2; ++r) {
                 st_s(o + F1 * r, V[w][r].x);
                 st_s(o + L + F1 * r, V[w][r].y);
             }
-#endif
         }
     });
-    drain_vm();  // the LDS-DMA warm loads land before the workgroup (and its LDS) is gone
+    drain_vm();  // the stores drain before the workgroup ends (measured free, r05: kept)
     __syncthreads();
     GD_TRACE(9);
 }
@@ -782,7 +653,6 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its update
     __shared__ float2 nyqh[L];      // the OTF's Nyquist column
     __shared__ float nyqo[L];       // x(., L/2)
-    __shared__ float4 pf_sink[64];  // warm_next's LDS-DMA target (never read)
     const int tid = threadIdx.x, line = tid / F1, j = tid - line * F1;
     const int g = blockIdx.x;
     const bool l0 = (line == 0);
@@ -805,7 +675,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             for (int r = 0; r < F2; ++r) X[q][r] = make_float2(fmaxf(r0[F1 * r], 0.f) * ial, fmaxf(r0[L + F1 * r], 0.f) * ial);
         }
     }
-    stagger_start<GD_INIT_STAGGER>(g);
+    stagger_start<GD_INIT_STAGGER>(g, a.N);
     __syncthreads();  // twiddles
     GD_TRACE(1);
 #pragma unroll
@@ -1016,7 +886,6 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
             }
         }
         for (int i = tid; i < L / 2; i += T) S[i * SLD + L / 2] = make_float2(nyqo[hf * L / 2 + i], 0.f);
-        warm_next<L, hf, 2>(a.y, g, a.N, pf_sink, tid, T);
         lds_barrier();
 #pragma unroll
         for (int w = 0; w < RG::HPL; ++w) {
@@ -1073,7 +942,7 @@ __global__ __launch_bounds__(512) void k_gal_reg_init(Args a) {
     // W: F(x0)'s columns -> W~ (no inverse)
     GD_TRACE(8);
     slices(std::false_type{});
-    drain_vm();  // the LDS-DMA warm loads land before the workgroup (and its LDS) is gone
+    drain_vm();  // the stores drain before the workgroup ends (measured free, r05: kept)
     __syncthreads();
     GD_TRACE(13);
 }

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             }
         }
     }
-    stagger_start<GD_RL_STAGGER>(g);
+    stagger_start<GD_RL_STAGGER>(g, a.N);
     __syncthreads();  // twiddles
     {
         const int line = tid / F1, j = tid - line * F1;

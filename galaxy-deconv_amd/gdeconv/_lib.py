@@ -13,7 +13,7 @@ import torch  # noqa: F401  (load torch's HIP runtime before dlopen of the engin
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgdeconv.so")
 
 GD_OK = 0
-ABI_VERSION = 4
+ABI_VERSION = 5
 GD_LLH = {"Gaussian": 0, "Poisson": 1}
 
 _P = ctypes.c_void_p

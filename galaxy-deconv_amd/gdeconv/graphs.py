@@ -5,12 +5,14 @@ a few hundred galaxies) one ``Unrolled_ADMM`` forward is a chain of ~60 short la
 OTF, init_l2, 8 x (denoiser, spectral iteration) - and the host, not the GPU, sets the pace.
 ``GraphedForward`` records the forward once into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm)
 and replays it: the engine's C ABI enqueues on torch's current stream and allocates nothing of its
-own.  Under capture its Infinity-Cache chunks are still pipelined onto the engine's internal streams
-(a fork / join per operation, each with its own captured event set, ``gd_set_capture_pipeline``);
-only an init that ``ADMMState.init_concurrent`` runs on a side stream keeps its chunks serial there:
-a fork nested inside that side stream's own fork was what crashed the ROCm 7 runtime when the graph
-was instantiated (``profiles/r04dbg_160_graph_crash.txt``, root cause in
-``profiles/r05b_capture_probe.txt``).
+own.  Under capture the engine runs an operation's Infinity-Cache chunks in sequence unless the caller
+opts in (``gd_set_capture_pipeline``, per host thread); ``GraphedForward`` opts in (``pipeline=True``), since
+it enqueues from the capturing stream itself: the chunks then fork onto capture streams of this host thread
+(never the internal streams other threads' eager calls use), a fork / join per operation with its own
+captured event set.  An init that ``ADMMState.init_concurrent`` runs on a side stream keeps its chunks serial
+there: a fork nested inside that side stream's own fork was what crashed the ROCm 7 runtime when the graph
+was instantiated (``profiles/r04dbg_160_graph_crash.txt``, ``profiles/r05b_capture_probe.txt``).
+A mode the caller set with ``gd_set_capture_pipeline`` before constructing is kept.
 
     g = GraphedForward(model, obs, psf, alpha)     # shapes fixed at capture
     rec = g(obs2, psf2, alpha2)                    # copies inputs in, replays, returns the output
@@ -22,7 +24,7 @@ import torch
 
 
 class GraphedForward:
-    def __init__(self, model, *example, warmup=2, clone=False):
+    def __init__(self, model, *example, warmup=2, clone=False, pipeline=True):
         for t in example:
             if not (torch.is_tensor(t) and t.is_cuda):
                 raise ValueError("GraphedForward captures device tensors only")
@@ -35,9 +37,17 @@ class GraphedForward:
             for _ in range(warmup):  # first calls build caches (folded BN, workspaces, MIOpen plans)
                 model(*self.static_in)
         torch.cuda.current_stream().wait_stream(side)
+        from . import _lib
+        lib = _lib.load()
+        prev = lib.gd_set_capture_pipeline(2 if pipeline else 0)
+        if prev != -1:                      # the caller chose a mode for this thread: keep it
+            lib.gd_set_capture_pipeline(prev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph):
-            self.static_out = model(*self.static_in)
+        try:
+            with torch.no_grad(), torch.cuda.graph(self.graph):
+                self.static_out = model(*self.static_in)
+        finally:
+            lib.gd_set_capture_pipeline(prev)
 
     def __call__(self, *inputs):
         if len(inputs) != len(self.static_in):

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GD_ABI_VERSION 4
+#define GD_ABI_VERSION 5  /* 5: strict 0 / 1 fused-path setters, capture pipelining opt-in (mode 1 gone) */
 
 #define GD_OK 0
 #define GD_ERR_ARG (-1)
@@ -219,24 +219,28 @@ int gd_admm_init_subnet(const float* y, const float* psf, long long psf_gstride,
 size_t gd_set_chunk_bytes(size_t bytes);
 int gd_set_pipeline_streams(int streams);
 
-/* Chunk pipelining under stream capture, for the CALLING HOST THREAD only: mode 2 (the default) forks a captured
- * operation's chunks onto the internal streams with an event set of its own, 0 runs them in sequence on the
- * capturing stream (use it when enqueuing from a stream that joined the capture through an event: such a nested
- * fork crashed the ROCm 7 runtime inside hipStreamEndCapture), 1 reuses one event set; -1 restores the default
- * (the GD_CAPTURE_PIPELINE environment variable, else 2).  Returns the previous override (-1: none). */
+/* Chunk pipelining under stream capture, for the CALLING HOST THREAD only: mode 0 (the default) runs a captured
+ * operation's chunks in sequence on the capturing stream; mode 2 forks them onto streams of the calling thread (never
+ * the internal streams eager calls of other threads use, since streams that join a capture stay in it until
+ * hipStreamEndCapture), each operation with an event set of its own.  Opt in to 2 only when enqueuing from the
+ * capturing stream itself (gdeconv.graphs.GraphedForward does): a fork from a stream that joined the capture through
+ * an event crashed the ROCm 7 runtime inside hipStreamEndCapture.  -1 restores the default (the GD_CAPTURE_PIPELINE
+ * environment variable, 0 or 2, else 0).  Returns the previous override (-1: none), or GD_ERR_UNSUPPORTED (setting
+ * unchanged) for any other mode. */
 int gd_set_capture_pipeline(int mode);
 
 /* Fused iterations: at the sizes that have them (see "sizes" above; Poisson at 256^2 and square L <= 112)
  * gd_admm_iter runs one workgroup per galaxy holding the galaxy's spectra on-chip (no workspace traffic).
- * on != 0 (default 1) selects them; 0 selects the chained path (row pass / column pass / row pass through
- * the workspace).  Returns the previous setting (0 or 1); process-wide. */
+ * on = 1 (default) selects them; 0 selects the chained path (row pass / column pass / row pass through
+ * the workspace).  Returns the previous setting (0 or 1), or GD_ERR_ARG (setting unchanged) for any other value;
+ * process-wide. */
 int gd_set_fused_iteration(int on);
 
 /* Richardson-Lucy at 256^2 (gd_richardson_lucy, models/Richard_Lucy.py:10-24): on = 1 (default) runs the
  * OTF, then the whole n_iters loop of each galaxy inside one 512-thread workgroup (k_rl_reg: the
  * galaxy's spectra stay on-chip; x, y and the OTF are re-read from the cache hierarchy); 0 selects the
- * chunked chain (four launches per iteration through the workspace).  Returns the previous setting;
- * process-wide. */
+ * chunked chain (four launches per iteration through the workspace).  Returns the previous setting (0 or 1), or
+ * GD_ERR_ARG (setting unchanged) for any other value; process-wide. */
 int gd_set_fused_rl(int on);
 
 /* SubNet from the PSFs (gd_subnet_rhos_psf): batches of at most n galaxies run features + MLP in ONE
@@ -249,11 +253,12 @@ int gd_set_subnet_fused_max(int n);
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->
- * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic (k_gal_reg_init).  on != 0
- * (default 1) selects it, 0 the chunked chain.  At the mid sizes (80 ... 160, multiples of 16) the one-launch
+ * |H|^2, G, x0 = clamp(X0) -> zin and F(x0) -> W~ with no workspace traffic (k_gal_reg_init).  on = 1
+ * (default) selects it, 0 the chunked chain.  At the mid sizes (80 ... 160, multiples of 16) the one-launch
  * k_gal_mid_init (the placed PSF's row spectra parked in the U1 slot, the half spectrum in LDS) runs when
  * BOTH this and gd_set_fused_iteration are on, in place of the RF_PSF_Y -> C_G_INIT -> RIF_CLAMP -> C_G_W1
- * chain.  Returns the previous setting (0 or 1); process-wide. */
+ * chain.  Returns the previous setting (0 or 1), or GD_ERR_ARG (setting unchanged) for any other value;
+ * process-wide. */
 int gd_set_fused_init(int on);
 
 /* Opt-in timing with hipEvents: level 1 brackets every whole operation (op_admm_init/op_admm_iter,

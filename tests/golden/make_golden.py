@@ -17,6 +17,8 @@ Fixtures (all fp32; complex stored as [..., 2] real/imag):
                        and per-iteration traces (v, z, x, zin); sample 0 = tutorial stamp
   admm256_id.npz   G3  Unrolled_ADMM(n=8) with denoiser = identity at 256^2, N=1, both llh
   wiener_rl.npz    G4  Wiener, Richard_Lucy(10), Richard_Lucy(100) at 48^2 (N=2) and 256^2 (N=1)
+  admm256.npz      G5  Unrolled_ADMM(n=2, 8; Gaussian, Poisson) at 256^2, N=2 (seeded), real ResUNet/SubNet
+                       with the generated weights: rhos, output and per-iteration traces (z, zin)
   state_dict_keys.json  the 98 keys + shapes of Unrolled_ADMM(n_iters=8)
 """
 import json
@@ -99,7 +101,7 @@ def run_admm(obs, psf, alpha, n, llh, identity=False, trace=False):
 
 
 def main(only=None):
-    """``only``: regenerate just that fixture ("otf_conv", "admm48", "admm256_id", "wiener_rl"); the others are
+    """``only``: regenerate just that fixture ("otf_conv", "admm48", "admm256_id", "admm256", "wiener_rl"); the others are
     left as committed (their arrays are deterministic, but a rewrite changes the zip's timestamps)."""
     torch.manual_seed(0)
     torch.set_num_threads(8)
@@ -139,6 +141,20 @@ def main(only=None):
             g3[f"{llh}_{k}"] = v
     if want("admm256_id"):
         np.savez_compressed(os.path.join(HERE, "admm256_id.npz"), **g3)
+
+    # G5: ADMM at 256^2 (configs[2]'s stamp), N=2, the real ResUNet / SubNet with the generated weights:
+    # per-iteration denoiser inputs (zin) and outputs (z) - z is the ResUNet's own tensor, never the buffer
+    # the engine writes zin to, so a replay pins k_gal_reg / the Poisson two-pass on the product path.
+    # v and x are not stored (not observable through the engine API; 256 KiB per galaxy-iteration each).
+    if want("admm256"):
+        obs, psf, alpha, _ = make_batch(2, 256, seed=256)
+        g5 = {"obs": obs.numpy(), "psf": psf.numpy(), "alpha": alpha.numpy()}
+        for llh in ("Gaussian", "Poisson"):
+            for n in (2, 8):
+                r = run_admm(obs, psf, alpha, n, llh, trace=True)
+                for k in ("out", "rho1", "rho2", "z", "zin"):
+                    g5[f"{llh}_n{n}_{k}"] = r[k]
+        np.savez_compressed(os.path.join(HERE, "admm256.npz"), **g5)
 
     # G4: Wiener and Richardson-Lucy
     g4 = {}

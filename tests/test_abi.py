@@ -50,7 +50,7 @@ def test_library_exports_every_header_symbol(lib):
 
 def test_host_only_queries(lib):
     from gdeconv import _lib as _lib_mod
-    assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 4
+    assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 5
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
     # other sizes up to 1638 per side, square or not, run the runtime-planned kernels (2)
     assert lib.gd_supported_size(50, 50) == 2 and lib.gd_supported_size(256, 128) == 2
@@ -64,6 +64,22 @@ def test_host_only_queries(lib):
     assert lib.gd_gx_state_bytes(2, 40, 56) == 2 * 57 * 80 * 12
     assert lib.gd_gx_state_bytes(2, 48, 48) == 2 * 49 * 96 * 12
     assert lib.gd_gx_state_bytes(2, 41, 56) == 0 and lib.gd_gx_state_bytes(2, 40, 513) == 0
+
+
+def test_switch_setters_are_strict(lib):
+    """ABI 5: the fused-path setters take 0 or 1 only, the capture pipelining mode -1, 0 or 2 only; anything else
+    is an error and leaves the setting unchanged (ABI 4 mapped any non-zero value to 1)."""
+    for name in ("gd_set_fused_iteration", "gd_set_fused_init", "gd_set_fused_rl"):
+        f = getattr(lib, name)
+        cur = f(1)
+        assert cur in (0, 1)
+        assert f(2) == -1 and f(3) == -1 and f(-5) == -1
+        assert f(cur) == 1, name              # still 1 after the refused values
+    assert lib.gd_set_capture_pipeline(1) == -2
+    prev = lib.gd_set_capture_pipeline(2)
+    assert prev in (-1, 0, 2)
+    assert lib.gd_set_capture_pipeline(0) == 2
+    assert lib.gd_set_capture_pipeline(prev) == 0
 
 
 def test_argument_errors_need_no_device(lib):

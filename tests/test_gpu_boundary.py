@@ -93,6 +93,81 @@ def test_two_host_threads_pipelined_calls(dev):
         lib.gd_set_chunk_bytes(old)
 
 
+def test_capture_pipeline_beside_eager_thread(dev):
+    """One host thread captures a chunk-pipelined forward (gd_set_capture_pipeline 2, GraphedForward's opt-in)
+    while a second thread runs eager chunk-pipelined calls INSIDE the capture window: the capture forks onto
+    streams of the capturing thread, never the internal streams the eager calls use, so the eager kernels are
+    not captured into the graph (nor invalidate it) and both results equal the serial ones bit for bit."""
+    import threading
+    from gdeconv import _lib, engine
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.models import Unrolled_ADMM
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    H = W = 100                                   # runtime-planned: chunked init / iterations
+    tgal = 2 * (W // 2 + 1) * H * 8
+    old = lib.gd_set_chunk_bytes(2 * tgal)
+    try:
+        obs, psf, alpha, _ = make_batch(7, H, W, seed=11, device=dev)
+        wo, wp, wa, _ = make_batch(9, H, W, seed=12, device=dev)
+        m = Unrolled_ADMM(n_iters=3, llh="Gaussian").to(dev).eval()
+        with torch.no_grad():
+            serial_w = engine.wiener(wo, wp, wa).clone()
+        torch.cuda.synchronize()
+        go, enq, ended = threading.Event(), threading.Event(), threading.Event()
+        res, errs = [], []
+        ws = torch.cuda.Stream(dev)
+
+        def worker():
+            try:
+                with torch.cuda.stream(ws):       # warm the worker stream's allocator blocks before the capture
+                    held = [engine.wiener(wo, wp, wa) for _ in range(3)]   # (no hipMalloc inside the window)
+                    del held
+                ws.synchronize()
+                go.wait(60)
+                with torch.cuda.stream(ws):
+                    for _ in range(3):
+                        res.append(engine.wiener(wo, wp, wa))
+                enq.set()
+                ended.wait(60)                     # no synchronising call while the capture is open
+                ws.synchronize()
+            except Exception as e:  # surfaced below
+                errs.append(e)
+                enq.set()
+
+        class Gate(torch.nn.Module):                # the denoiser: holds the capture open while the worker enqueues
+            def __init__(self):
+                super().__init__()
+                self.armed = False
+
+            def forward(self, z):
+                if self.armed and torch.cuda.is_current_stream_capturing():
+                    self.armed = False
+                    go.set()
+                    enq.wait(60)
+                return z
+
+        m.Z = Gate()
+        with torch.no_grad():
+            eager = m(obs, psf, alpha).clone()   # (the gate is the identity outside a capture)
+        t = threading.Thread(target=worker)
+        t.start()
+        m.Z.armed = True
+        try:
+            g = GraphedForward(m, obs, psf, alpha, clone=True)
+        finally:
+            go.set()
+            ended.set()
+            t.join(120)
+        assert not errs, errs
+        assert len(res) == 3
+        for r in res:
+            assert torch.equal(r, serial_w)
+        assert torch.equal(g(obs, psf, alpha), eager)
+    finally:
+        lib.gd_set_chunk_bytes(old)
+
+
 def test_conv_fft_batch_shared_otf_broadcasts(dev):
     """conv_fft_batch(H, x) with ONE [1,1,H,W] OTF for N images (the reference's fftn(x) * H broadcast,
     utils/utils_torch.py:46-50): equal to the expanded per-galaxy OTF bit for bit, and to the oracle."""

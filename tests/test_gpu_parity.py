@@ -325,6 +325,59 @@ def test_admm48_full_model_drop_in(dev, llh, n):
     assert e < TOL
 
 
+@pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
+@pytest.mark.parametrize("n", [2, 8])
+def test_admm256_replay_reference_denoiser(dev, llh, n, fused):
+    """configs[2]'s kernels on their product path: at 256^2 (k_gal_reg / k_gal_reg_init for Gaussian, the
+    Poisson two-pass k_gal_reg<POIS> + k_pois_b, or the three-kernel chain with fused=0) the reference's own
+    per-iteration ResUNet outputs z are fed back as tensors of their own (never the zin buffer the engine
+    writes, unlike the identity-denoiser tests where z IS zin), and every iteration's denoiser input and
+    the output are checked against the reference's (models/Unrolled_ADMM.py:199-215), N = 2 galaxies."""
+    g = golden("admm256.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    zs, zins = T(g[f"{llh}_n{n}_z"]), T(g[f"{llh}_n{n}_zin"])
+    seen, fed = [], []
+
+    class Replay(torch.nn.Module):
+        def forward(self, zin):
+            seen.append(zin.detach().cpu().clone())
+            z = zs[len(seen) - 1].to(zin.device)
+            fed.append(z)
+            assert z.data_ptr() != zin.data_ptr()
+            return z
+
+    m = _spectral_model(n, llh, dev, T(g[f"{llh}_n{n}_rho1"]), T(g[f"{llh}_n{n}_rho2"]))
+    m.Z = Replay()
+    with torch.no_grad():
+        out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    assert len(seen) == n
+    for it in range(n):
+        assert nerr(seen[it], zins[it]) < TOL, f"denoiser input of iteration {it}"
+        assert torch.equal(fed[it].cpu(), zs[it]), f"the engine wrote into z of iteration {it}"
+    assert report(f"admm 256^2 n={n} {llh} reference-denoiser replay, fused={fused}", out,
+                  T(g[f"{llh}_n{n}_out"])) < TOL
+
+
+@pytest.mark.parametrize("llh,n", [("Gaussian", 2), ("Gaussian", 8), ("Poisson", 2), ("Poisson", 8)])
+def test_admm256_full_model_drop_in(dev, llh, n):
+    """configs[2]'s stamp end to end: the drop-in Unrolled_ADMM (HIP spectral path + SubNet engine + PyTorch
+    ResUNet on the GPU) with the deterministic weights vs the reference on CPU, N = 2 at 256^2."""
+    from gdeconv.weights import make_state_dict
+    from models.Unrolled_ADMM import Unrolled_ADMM
+    g = golden("admm256.npz")
+    m = Unrolled_ADMM(n_iters=n, llh=llh)
+    m.load_state_dict(make_state_dict(m, WEIGHT_SEED))
+    m = m.to(dev).eval()
+    obs, psf, alpha = (T(g[k]).to(dev) for k in ("obs", "psf", "alpha"))
+    with torch.no_grad():
+        r1, r2 = m.init(psf, alpha)
+        out = m(obs, psf, alpha).cpu()
+    assert nerr(r1.reshape(2, -1).cpu(), T(g[f"{llh}_n{n}_rho1"]).reshape(2, -1)) < TOL
+    assert nerr(r2.reshape(2, -1).cpu(), T(g[f"{llh}_n{n}_rho2"]).reshape(2, -1)) < TOL
+    e = report(f"Unrolled_ADMM 256^2 n={n} {llh} full model (configs[2] stamp)", out, T(g[f"{llh}_n{n}_out"]))
+    assert e < TOL
+
+
 def test_configs1_full_batch_48(dev):
     """configs[1] at its real batch: Unrolled_ADMM(n_iters=8, Gaussian) on 256 galaxies of 48^2 (full
     model: SubNet + ResUNet on the GPU).  Batch invariance (each galaxy as in a 3-galaxy batch, bit for

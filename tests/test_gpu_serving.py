@@ -57,8 +57,9 @@ def test_graphed_forward_engine_bit_identical(dev, L, N, llh):
 def test_graphed_forward_chunked_pipeline(dev, H, W, mode):
     """A forward whose runtime-planned operations run in several Infinity-Cache chunks (chunk bytes
     forced down to two galaxies; the 4096 x 160^2 bench line did the same at 96 MiB before 160^2 was fused)
-    captures and replays bit-identically, with the chunks pipelined over the internal streams under capture
-    (gd_set_capture_pipeline 2, the default: an event set per operation) or in sequence (0)."""
+    captures and replays bit-identically, with the chunks pipelined over the capturing thread's streams under
+    capture (gd_set_capture_pipeline 2, GraphedForward's opt-in: an event set per operation) or in sequence (0,
+    the engine's default; a mode the caller set is kept by GraphedForward)."""
     from gdeconv import _lib
     from gdeconv.graphs import GraphedForward
     from gdeconv.synth import make_batch

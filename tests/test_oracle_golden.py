@@ -79,6 +79,36 @@ def test_admm48_full_model(llh, n):
         assert torch.equal(torch.stack(trace["x"][1:]), T(g[f"{llh}_n{n}_x"]))
 
 
+@pytest.mark.parametrize("llh,n", [("Gaussian", 2), ("Gaussian", 8), ("Poisson", 2), ("Poisson", 8)])
+def test_admm256_reference_denoiser_trace(llh, n):
+    """admm256.npz (256^2, N=2, real ResUNet): the SubNet mirror gives the reference's rhos and the oracle,
+    fed the reference's per-iteration denoiser outputs, reproduces every denoiser input and the output bit
+    for bit; n = 2 also end to end through the host ResUNet mirror."""
+    torch.set_num_threads(8)
+    g = golden("admm256.npz")
+    obs, psf, alpha = T(g["obs"]), T(g["psf"]), T(g["alpha"])
+    zs = T(g[f"{llh}_n{n}_z"])
+    m = _denoiser_and_subnet(n)
+    seen = []
+
+    def replay(zin):
+        seen.append(zin.clone())
+        return zs[len(seen) - 1]
+
+    with torch.no_grad():
+        rho1, rho2 = m.init(psf, alpha)
+        assert torch.equal(rho1, T(g[f"{llh}_n{n}_rho1"]))
+        assert torch.equal(rho2, T(g[f"{llh}_n{n}_rho2"]))
+        out = O.admm_forward(obs, psf, alpha, rho1, rho2, llh, denoise=replay)
+        assert torch.equal(out, T(g[f"{llh}_n{n}_out"]))
+        assert torch.equal(torch.stack(seen), T(g[f"{llh}_n{n}_zin"]))
+        if n == 2:
+            trace = {}
+            out = O.admm_forward(obs, psf, alpha, rho1, rho2, llh, denoise=m.Z, trace=trace)
+            assert torch.equal(out, T(g[f"{llh}_n{n}_out"]))
+            assert torch.equal(torch.stack(trace["z"]), zs)
+
+
 @pytest.mark.parametrize("llh", ["Gaussian", "Poisson"])
 def test_admm48_xdenseunet_denoiser(llh):
     """Unrolled_ADMM(denoiser='XDenseUNet') (models/Unrolled_ADMM.py:142-151, :163): the oracle + the
