@@ -12,7 +12,9 @@ it enqueues from the capturing stream itself: the chunks then fork onto capture 
 captured event set.  An init that ``ADMMState.init_concurrent`` runs on a side stream keeps its chunks serial
 there: a fork nested inside that side stream's own fork was what crashed the ROCm 7 runtime when the graph
 was instantiated (``profiles/r04dbg_160_graph_crash.txt``, ``profiles/r05b_capture_probe.txt``).
-A mode the caller set with ``gd_set_capture_pipeline`` before constructing is kept.
+A mode the caller set with ``gd_set_capture_pipeline`` before constructing is kept.  A server whose other host
+threads keep launching work while one thread captures passes ``capture_error_mode="thread_local"`` (torch's
+default "global" mode invalidates the capture on another thread's potentially unsafe call).
 
     g = GraphedForward(model, obs, psf, alpha)     # shapes fixed at capture
     rec = g(obs2, psf2, alpha2)                    # copies inputs in, replays, returns the output
@@ -24,7 +26,7 @@ import torch
 
 
 class GraphedForward:
-    def __init__(self, model, *example, warmup=2, clone=False, pipeline=True):
+    def __init__(self, model, *example, warmup=2, clone=False, pipeline=True, capture_error_mode="global"):
         for t in example:
             if not (torch.is_tensor(t) and t.is_cuda):
                 raise ValueError("GraphedForward captures device tensors only")
@@ -44,7 +46,7 @@ class GraphedForward:
             lib.gd_set_capture_pipeline(prev)
         self.graph = torch.cuda.CUDAGraph()
         try:
-            with torch.no_grad(), torch.cuda.graph(self.graph):
+            with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=capture_error_mode):
                 self.static_out = model(*self.static_in)
         finally:
             lib.gd_set_capture_pipeline(prev)

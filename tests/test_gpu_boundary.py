@@ -97,7 +97,9 @@ def test_capture_pipeline_beside_eager_thread(dev):
     """One host thread captures a chunk-pipelined forward (gd_set_capture_pipeline 2, GraphedForward's opt-in)
     while a second thread runs eager chunk-pipelined calls INSIDE the capture window: the capture forks onto
     streams of the capturing thread, never the internal streams the eager calls use, so the eager kernels are
-    not captured into the graph (nor invalidate it) and both results equal the serial ones bit for bit."""
+    not captured into the graph (nor invalidate it) and both results equal the serial ones bit for bit.  (The
+    capture runs in torch's "thread_local" error mode: in "global" mode any potentially unsafe call of the other
+    thread, the caching allocator's included, invalidates it whatever the engine does.)"""
     import threading
     from gdeconv import _lib, engine
     from gdeconv.graphs import GraphedForward
@@ -154,7 +156,7 @@ def test_capture_pipeline_beside_eager_thread(dev):
         t.start()
         m.Z.armed = True
         try:
-            g = GraphedForward(m, obs, psf, alpha, clone=True)
+            g = GraphedForward(m, obs, psf, alpha, clone=True, capture_error_mode="thread_local")
         finally:
             go.set()
             ended.set()
