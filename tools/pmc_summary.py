@@ -100,6 +100,32 @@ def per_launch(path, counter):
     return {k: sum(v) / len(v) for k, v in by_k.items()}, {k: len(v) for k, v in by_k.items()}
 
 
+def dispatch_order(path, counter):
+    """[(dispatch id, kernel, value)] of one counter pass in dispatch order (every profiled engine kernel)."""
+    sums = collections.defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        name = pretty(r.get("Kernel_Name", ""))
+        if name:
+            sums[(int(r.get("Dispatch_Id")), name)] += float(r["Counter_Value"])
+    return [(d, k, v) for (d, k), v in sorted(sums.items())]
+
+
+def init_pass_b(path, counter, L):
+    """Mean per launch of the Poisson init's own pass B (k_pois_b<INIT>: the k_pois_b dispatch that follows a
+    k_gal_reg_init<POIS> dispatch) and of the iterations' pass B, from one counter pass; None when absent."""
+    seq = dispatch_order(path, counter)
+    ini, it = [], []
+    for i, (_, k, v) in enumerate(seq):
+        if k != f"k_pois_b<{L}>":
+            continue
+        (ini if i > 0 and seq[i - 1][1] == f"k_gal_init<{L},POIS>" else it).append(v)
+    if not ini:
+        return None
+    return sum(ini) / len(ini), (sum(it) / len(it) if it else 0.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
@@ -164,12 +190,31 @@ def main():
             "launches": a.iters, "note": "Poisson two-pass: pass A + pass B per call (the init's pass B excluded)"}
     if f"k_gal_init<{L},POIS>" in out["kernels"] and f"k_pois_b<{L}>" in out["kernels"]:
         pi = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},POIS>"]
+        # the init's pass B (k_pois_b<INIT>: no w read) apart from the iterations' (w read): round 5 priced the init
+        # with the average over both, i.e. (n - 1) / n of an image too many (the 1.10x "excess" of
+        # profiles/r05i_pmc_summary_poisson.txt was that accounting)
+        fb, wb = init_pass_b(a.fetch, "FETCH_SIZE", L), init_pass_b(a.write, "WRITE_SIZE", L)
+        if fb and wb:
+            pb_init, pb_iter = 2 * fb[0] * 1024 + wb[0] * 1024, 2 * fb[1] * 1024 + wb[1] * 1024
+            ni = out["kernels"][f"k_gal_init<{L},POIS>"]["launches"]
+            nb = out["kernels"][f"k_pois_b<{L}>"]["launches"]
+            out["kernels"][f"k_pois_b<{L},INIT>"] = {"hbm_bytes_per_launch": pb_init, "launches": ni}
+            out["kernels"][f"k_pois_b<{L},ITER>"] = {"hbm_bytes_per_launch": pb_iter, "launches": nb - ni}
+            pa = out["kernels"].get(f"k_pois_a<{L}>")
+            if pa and f"op_admm_iter<{L},Poisson>" in out["kernels"]:
+                it = out["kernels"][f"op_admm_iter<{L},Poisson>"]["launches"]
+                out["kernels"][f"op_admm_iter<{L},Poisson>"]["hbm_bytes_per_launch"] = \
+                    (pa["hbm_bytes_per_launch"] * pa["launches"] + pb_iter * (nb - ni)) / it
+                out["kernels"][f"op_admm_iter<{L},Poisson>"]["note"] = \
+                    "Poisson two-pass: pass A + the iterations' pass B per call (the init's pass B apart)"
+            note = "k_psf_rows<STATE> + k_gal_reg_init<POIS> + the init's own pass B (k_pois_b<INIT>)"
+        else:
+            pb_init = out["kernels"][f"k_pois_b<{L}>"]["hbm_bytes_per_launch"]
+            note = "k_psf_rows<STATE> + k_gal_reg_init<POIS> + one pass B (its per-launch average)"
         out["kernels"][f"op_admm_init<{L},Poisson>"] = {
             "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch"] for k in pi if k in out["kernels"])
-            + out["kernels"][f"k_pois_b<{L}>"]["hbm_bytes_per_launch"],
-            "launches": out["kernels"][f"k_gal_init<{L},POIS>"]["launches"],
-            "note": "Poisson init: k_psf_rows<STATE> + k_gal_reg_init<POIS> + one pass B (its per-launch average "
-                    "over the init's and the iterations' launches)"}
+            + pb_init,
+            "launches": out["kernels"][f"k_gal_init<{L},POIS>"]["launches"], "note": "Poisson init: " + note}
     init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},Y>", f"k_gal_init<{L},W1>"]
     if f"k_gal_init<{L},ONE>" in out["kernels"]:
         init = [f"k_psf_rows<{L},STATE>", f"k_gal_init<{L},ONE>"]
