@@ -3042,6 +3042,15 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
     return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_iter(a, (hipStream_t)stream); });
 }
 
+int gd_admm_iter_v(const long long* v) {
+    if (v == nullptr) return fail(GD_ERR_ARG, "gd_admm_iter_v: null argument vector");
+    const auto p = [v](int i) { return reinterpret_cast<void*>(static_cast<intptr_t>(v[i])); };
+    return gd_admm_iter(static_cast<const float*>(p(0)), static_cast<const float*>(p(1)), static_cast<float*>(p(2)),
+                        static_cast<const float*>(p(3)), v[4], static_cast<const float*>(p(5)), v[6],
+                        static_cast<const float*>(p(7)), v[8], static_cast<const float*>(p(9)), v[10], (int)v[11],
+                        (int)v[12], (int)v[13], (int)v[14], (int)v[15], (int)v[16], p(17), p(18), p(19));
+}
+
 int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,
               long long alpha_stride, float* x, int N, int H, int W, void* ws, void* stream) {
     GD_TRY(check_shape(N, H, W));

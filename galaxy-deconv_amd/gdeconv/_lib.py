@@ -41,6 +41,7 @@ SIGNATURES = {
     "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P]),
     "gd_admm_iter": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P,
                           _P]),
+    "gd_admm_iter_v": (_I, [_P]),
     "gd_wiener": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _I, _I, _I, _P, _P]),
     "gd_richardson_lucy": (_I, [_P, _P, _LL, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P]),
     "gd_tikhonov": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _P, _LL, _P, _I, _I, _I, _P, _P]),

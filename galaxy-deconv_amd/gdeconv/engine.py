@@ -18,6 +18,7 @@ the caller's current device is.  Scratch workspaces come from torch's caching al
 (on that stream), so calls on different streams or threads never share scratch memory.
 """
 import contextlib
+import ctypes
 
 import torch
 
@@ -570,6 +571,8 @@ class ADMMState:
         self._fixed = (self.y.data_ptr(), self.alpha.data_ptr(), self.alpha_s, self.state.data_ptr(),
                        self.ws.data_ptr())
         self._dev_index = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        self._shape = tuple(self.y.shape)
+        self._bind()
         self.layout = None
         self.iter = 0
         self._side = None   # the side stream an init_concurrent() is running on, until joined
@@ -677,6 +680,18 @@ class ADMMState:
             torch.cuda.current_stream(self.dev).wait_stream(self._side)
             self._side = None
 
+    def _bind(self):
+        """The packed argument vector of gd_admm_iter_v (its 20 slots in gd_admm_iter's order): the slots fixed for
+        this state (y, alpha, llh, N, H, W, state, workspace) set here from ``_fixed``, the per-call ones by ``step``
+        (one 1-argument ctypes call per iteration instead of 20 converted arguments: the eager 256 x 48^2 forward is
+        host-bound).  Call again after re-pointing ``_fixed``."""
+        yp, ap, as_, sp, wp = self._fixed
+        v = self._argv = (ctypes.c_longlong * 20)()
+        v[0], v[3], v[4], v[11] = yp, ap, as_, self.llh
+        v[14], v[15], v[16], v[17], v[18] = self.N, self.H, self.W, sp, wp
+        self._argv_addr = ctypes.addressof(v)
+        self._iter_v = self.lib.gd_admm_iter_v
+
     def step(self, z, rho1, rho2, rho2_next, out=None):
         """One loop body (models/Unrolled_ADMM.py:207-213) after the denoiser returned ``z``.
         ``rho*`` are (tensor or device pointer, stride) pairs (``RhoSchedule`` items); ``rho2_next`` None
@@ -687,13 +702,13 @@ class ADMMState:
             self.join()
         if z.dtype != torch.float32 or not z.is_contiguous():
             z = z.float().contiguous()
-        if z.shape != self.y.shape:
-            raise ValueError(f"denoiser returned {tuple(z.shape)}, expected {tuple(self.y.shape)}")
+        if z.shape != self._shape:
+            raise ValueError(f"denoiser returned {tuple(z.shape)}, expected {self._shape}")
         if z.device != self.dev:
             raise ValueError(f"denoiser returned a tensor on {z.device}, the state is on {self.dev}")
         last = rho2_next is None
         if last:
-            if out is None or out.shape != self.y.shape or out.dtype != torch.float32 or out.device != self.dev \
+            if out is None or out.shape != self._shape or out.dtype != torch.float32 or out.device != self.dev \
                     or not out.is_contiguous():
                 raise ValueError("the last iteration needs a contiguous fp32 `out` shaped like y on the state's device")
             dst = out
@@ -702,18 +717,23 @@ class ADMMState:
         if self.llh != 0 and self.lib.gd_admm_state_layout(self.H, self.W, self.llh) != self.layout:
             raise _lib.EngineError("the ADMM state layout changed since init (gd_set_fused_iteration toggled "
                                    "between gd_admm_init and gd_admm_iter)")
-        r1, r1s = _scalar_arg(rho1, self.dev)
-        r2, r2s = _scalar_arg(rho2, self.dev)
-        rn, rns = (None, 0) if last else _scalar_arg(rho2_next, self.dev)
-        yp, ap, as_, sp, wp = self._fixed
-        args = (yp, z.data_ptr(), dst.data_ptr(), ap, as_, r1, r1s, r2, r2s, rn, rns, self.llh, self.iter, int(last),
-                self.N, self.H, self.W, sp, wp)
+        v = self._argv
+        v[5], v[6] = _scalar_arg(rho1, self.dev)
+        v[7], v[8] = _scalar_arg(rho2, self.dev)
+        if last:
+            v[9], v[10] = 0, 0
+        else:
+            v[9], v[10] = _scalar_arg(rho2_next, self.dev)
+        v[1], v[2], v[12], v[13] = z.data_ptr(), dst.data_ptr(), self.iter, last
         if _current_device() == self._dev_index:
-            rc = self.lib.gd_admm_iter(*args, _stream(self.dev))
+            v[19] = _stream(self.dev) or 0
+            rc = self._iter_v(self._argv_addr)
         else:
             with _on(self.dev):
-                rc = self.lib.gd_admm_iter(*args, _stream(self.dev))
-        _lib.check(rc, "gd_admm_iter")
+                v[19] = _stream(self.dev) or 0
+                rc = self._iter_v(self._argv_addr)
+        if rc:
+            _lib.check(rc, "gd_admm_iter")
         self.iter += 1
         return dst
 

@@ -23,6 +23,7 @@
  *   gd_rfft2/gd_irfft2  utils/utils_torch.py:22-27   fftn / ifftn over dims [2,3] (real input, half spectrum)
  *   gd_admm_init        models/Unrolled_ADMM.py:181-196 + init_l2 :170-175 (+ first V step of :207)
  *   gd_admm_iter        models/Unrolled_ADMM.py:199-214 loop body around the denoiser call :208
+ *   gd_admm_iter_v      the same, arguments packed (interpreted callers)
  *                       (X_Update :315-319, V_Update_{Poisson,Gaussian} :326-328/:335-336, duals
  *                       :212-213, next V step, output scaling :215)
  *   gd_wiener           models/Wiener.py:10-20       Wiener.forward(y, psf, alpha)
@@ -121,6 +122,11 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
                  const float* rho1, long long rho1_stride, const float* rho2, long long rho2_stride,
                  const float* rho2_next, long long rho2_next_stride, int llh, int iter, int last, int N, int H,
                  int W, void* state, void* ws, void* stream);
+/* gd_admm_iter with its 20 arguments packed in that order into one int64 array (pointers and strides as
+ * integers, the int arguments widened): same semantics and return codes.  For interpreted callers whose
+ * per-argument conversion costs more than the call (Python ctypes: 2.9 us for the 20-argument call, 0.6 us for a
+ * short one) - at 256 x 48^2 the host sets the pace of an eager forward (gdeconv.engine.ADMMState.step). */
+int gd_admm_iter_v(const long long* argv);
 
 /* x = Re IFFT2(conj(H) FFT2(y) / (|H|^2 + 350/alpha)). */
 int gd_wiener(const float* y, const float* psf, long long psf_gstride, int h, int w, const float* alpha,

@@ -51,6 +51,7 @@ def main():
         st.state = arena[state_off:state_off + sbytes]
         st.zin = arena[zin_off:zin_off + img].view(torch.float32).view(N, 1, L, L)
         st._fixed = (st._fixed[0], st._fixed[1], st._fixed[2], st.state.data_ptr(), st._fixed[4])
+        st._bind()
         with torch.no_grad():
             st.init(None)
             z = st.zin if z_off is None else arena[z_off:z_off + img].view(torch.float32).view(N, 1, L, L)
