@@ -262,9 +262,12 @@ struct RegGeo {
 #endif
 // Only when the launch spans more than one round of workgroups (N > 256 galaxies at one per CU): a single round has
 // no later rounds to phase-lock, and its staggered groups would only start late.
+#ifndef GD_STAGGER_MIN_N
+#define GD_STAGGER_MIN_N 256  // launches of at most this many galaxies start unstaggered (0: every launch, round 5)
+#endif
 template <int US>
 __device__ __forceinline__ void stagger_start(int g, int N) {
-    if (US > 0 && N > 256 && g < 256 && (g % GD_STAGGER_N) != 0) {
+    if (US > 0 && N > GD_STAGGER_MIN_N && g < 256 && (g % GD_STAGGER_N) != 0) {
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         const unsigned long long d = (unsigned long long)US * 100 * (g % GD_STAGGER_N) / GD_STAGGER_N;
         while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(32);
