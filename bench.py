@@ -264,6 +264,8 @@ def parse():
                    help="Gaussian init: 1 the one-launch kernels (256^2: k_psf_rows + k_gal_reg_init), 0 the chunked chain")
     p.add_argument("--fused", type=int, default=None,
                    help="iterations: 1 the one-launch kernels (256^2: k_gal_reg), 0 the chained path")
+    p.add_argument("--fused-rl", type=int, default=None,
+                   help="Richardson-Lucy at 256^2: 1 k_rl_reg (the whole loop per galaxy), 0 the chunked chain")
     p.add_argument("--settle-s", type=float, default=2.0,
                    help="after the warmup steps, untimed steps until this many seconds of load (clock settling)")
     p.add_argument("--no-extra", action="store_true",
@@ -425,6 +427,8 @@ def measure(args, ctx):
         lib.gd_set_fused_iteration(args.fused)
     if args.fused_init is not None:
         lib.gd_set_fused_init(args.fused_init)
+    if args.fused_rl is not None:
+        lib.gd_set_fused_rl(args.fused_rl)
     fused_init = lib.gd_set_fused_init(1)
     lib.gd_set_fused_init(fused_init)
     fused = lib.gd_set_fused_iteration(0)
@@ -433,7 +437,13 @@ def measure(args, ctx):
     # 80 / 112 / 144 / 160 (runtime-planned sizes) and 96 / 128 run their Gaussian iterations and init fused too
     # (k_gal_mid, k_gal_mid_init: gd_engine.hip mid_size, GD_MID_EXTRA)
     mid_fused = bool(fused) and args.size in (80, 96, 112, 128, 144, 160) and args.llh == "Gaussian"
-    use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian"
+    # 256^2 Gaussian batches below gd_set_fused_min_batch run the chained kernels (one-workgroup-per-galaxy launches
+    # of fewer than ~a round of workgroups leave most CUs idle)
+    min_batch = lib.gd_set_fused_min_batch(-1)
+    small_chained = args.size == 256 and args.llh == "Gaussian" and args.batch < min_batch
+    use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian" and not small_chained
+    if small_chained:
+        fused_init = 0
     pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
     # Poisson at L <= 112: one workgroup per galaxy, both images in LDS (k_pois_small, k_pois_small_init)
     pois_small = bool(fused) and args.llh == "Poisson" and args.size in (32, 48, 64, 80, 96, 112)
@@ -701,7 +711,9 @@ def measure(args, ctx):
                                                     else (f"fused, k_pois_small ({L}^2: both images in LDS, one workgroup "
                                                           "per galaxy)") if pois_small
                                                     else "three-kernel, runtime-planned line FFTs (gd_generic.hpp)"
-                                                    if generic else "three-kernel")),
+                                                    if generic else
+                                                    f"three-kernel (batch below gd_set_fused_min_batch = {min_batch})"
+                                                    if small_chained else "three-kernel")),
                    "init": (None if rl else
                             ("fused, " + INIT_IMPL[fused_init] if fused_init else "chunked")
                             if (L == 256 and args.llh == "Gaussian") else

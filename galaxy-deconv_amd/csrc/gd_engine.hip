@@ -2321,6 +2321,11 @@ int g_fused_rl = 1;    // Richardson-Lucy at 256^2: 1 = k_rl_reg (whole loop per
 int g_subnet_fused_max = 256;
 int g_sri_map = 0;  // k_subnet_rhos_init's block -> (role, galaxy) map (tools/kbench_small)
 int g_fused_init = 1;  // Gaussian init (256^2: k_psf_rows<STATE> + k_gal_reg_init) and the other one-launch inits: 1 on; 0 = chunked
+// 256^2 Gaussian: the whole-galaxy kernels (k_gal_reg, k_psf_rows + k_gal_reg_init) from this batch up; smaller batches
+// run the chained row / column kernels, whose many small workgroups use the CUs a one-workgroup-per-galaxy launch of
+// N < 256 leaves idle (r06j: N = 1 2.1x, 8 2.1x, 32 1.62x, 64 1.28x faster chained; 128 1.17x, 256 1.82x faster fused).
+// The Gaussian state layout is the same either way, so the choice is per call.
+int g_fused_min_n = 96;
 
 // Eager pipelined operations fork onto the device's internal streams (PipeRes, shared by the host threads, one
 // operation at a time under its mutex).  Under stream capture (mode 2, gd_set_capture_pipeline) an operation
@@ -2611,7 +2616,7 @@ struct Ops {
             if (g_fused) return Lc::gal_small_init(a0, st0);  // both spectra in LDS, one pass
         }
         if constexpr (has_fused<L>()) {
-            if (g_fused_init && a0.h <= 64) {  // whole-galaxy passes, no workspace: PSF rows -> U1 slot, init, W~
+            if (g_fused_init && a0.h <= 64 && a0.N >= g_fused_min_n) {  // whole-galaxy passes, no workspace: PSF rows -> U1 slot, init, W~
                 GD_TRY(Lc::psf_rows_state(a0, st0));
                 return Lc::gal_reg_init(a0, st0);
             }
@@ -2630,7 +2635,7 @@ struct Ops {
     static int admm_iter_gauss(Args a, hipStream_t st0) {
         // a.a0 = z; spectral state updated in place; a.o0 = zin (or the output on the last iteration)
         if constexpr (has_fused<L>()) {
-            if (g_fused) return Lc::gal_reg(a, st0);  // one pass, no workspace
+            if (g_fused && a.N >= g_fused_min_n) return Lc::gal_reg(a, st0);  // one pass, no workspace
         }
         if constexpr (GD_MID_EXTRA && (L == 96 || L == 128)) {
             if (g_fused) return gal_mid_launch_t<L>(a, st0);  // k_gal_mid
@@ -3259,6 +3264,12 @@ int gd_set_fused_rl(int on) {
     if (on != 0 && on != 1) return fail(GD_ERR_ARG, "gd_set_fused_rl: 0 or 1");
     const int old = g_fused_rl;
     g_fused_rl = on;
+    return old;
+}
+
+int gd_set_fused_min_batch(int n) {
+    const int old = g_fused_min_n;
+    if (n >= 0) g_fused_min_n = n;
     return old;
 }
 

@@ -59,6 +59,7 @@ SIGNATURES = {
     "gd_set_fused_rl": (_I, [_I]),
     "gd_set_subnet_fused_max": (_I, [_I]),
     "gd_set_fused_init": (_I, [_I]),
+    "gd_set_fused_min_batch": (_I, [_I]),
     "gd_subnet_param_count": (_I, []),
     "gd_subnet_features": (_I, [_P, _P, _P, _I, _P]),
     "gd_subnet_mlp_param_count": (_I, [_I]),

@@ -256,6 +256,12 @@ int gd_set_fused_rl(int on);
  * previous value. */
 int gd_set_subnet_fused_max(int n);
 
+/* 256^2 Gaussian: batches of at least n galaxies run the whole-galaxy kernels (k_gal_reg, the one-launch init) when
+ * those are on; smaller batches run the chained row / column kernels, whose many small workgroups fill the CUs that
+ * one workgroup per galaxy leaves idle below a round of workgroups (the same state layout: chosen per call, results
+ * within rounding).  Default 96; n < 0 only queries.  Returns the previous value; process-wide. */
+int gd_set_fused_min_batch(int n);
+
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side
  * <= 64) the PSF's row spectra go into the state's U1 slot, then one workgroup per galaxy runs y ->

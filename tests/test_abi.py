@@ -75,6 +75,7 @@ def test_switch_setters_are_strict(lib):
         assert cur in (0, 1)
         assert f(2) == -1 and f(3) == -1 and f(-5) == -1
         assert f(cur) == 1, name              # still 1 after the refused values
+    assert lib.gd_set_fused_min_batch(-1) == 96     # 256^2 Gaussian: chained kernels below one round's worth
     assert lib.gd_set_capture_pipeline(1) == -2
     prev = lib.gd_set_capture_pipeline(2)
     assert prev in (-1, 0, 2)

@@ -3,6 +3,8 @@ vectors.  Bar: per galaxy max|out - ref| <= 1e-5 * max|ref| (fp
 
 Run on the MI355X box:  python -m pytest tests -m gpu -x -q
 """
+import contextlib
+
 import numpy as np
 import pytest
 import torch
@@ -167,14 +169,28 @@ def _spectral_model(n, llh, dev, rho1, rho2):
     return m
 
 
+@contextlib.contextmanager
+def _whole_galaxy_kernels_at_any_batch():
+    """256^2 routes batches below gd_set_fused_min_batch (96) to the chained kernels; tests that exercise the
+    whole-galaxy kernels on small batches lift that threshold."""
+    from gdeconv import _lib
+    lib = _lib.load()
+    old = lib.gd_set_fused_min_batch(0)
+    try:
+        yield
+    finally:
+        lib.gd_set_fused_min_batch(old)
+
+
 @pytest.fixture(params=[1, 0], ids=["fused_reg", "three_kernel"])
 def fused(request):
-    """Iterations through the one-kernel whole-galaxy path (256^2: k_gal_reg, the default) or the
-    three-kernel path."""
+    """Iterations through the one-kernel whole-galaxy path (256^2: k_gal_reg, the default from 96 galaxies, here
+    at every batch) or the three-kernel path."""
     from gdeconv import _lib
     lib = _lib.load()
     old = lib.gd_set_fused_iteration(request.param)
-    yield request.param
+    with _whole_galaxy_kernels_at_any_batch():
+        yield request.param
     lib.gd_set_fused_iteration(old)
 
 
@@ -239,7 +255,7 @@ def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
     m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
     old = lib.gd_set_fused_iteration(variant)
     try:
-        with torch.no_grad():
+        with torch.no_grad(), _whole_galaxy_kernels_at_any_batch():
             out_f = m(obs, psf, alpha).cpu()
             lib.gd_set_fused_iteration(0)
             out_t = m(obs, psf, alpha).cpu()
@@ -249,6 +265,38 @@ def test_fused_iteration_matches_three_kernel_path(dev, n, variant):
     idx = [0, 17, 36]
     ref = O.admm_forward(obs[idx].cpu(), psf[idx].cpu(), alpha[idx].cpu(), rho1[idx].cpu(), rho2[idx].cpu())
     assert nerr(out_f[idx], ref) < TOL
+
+
+@pytest.mark.parametrize("N", [1, 37, 95, 96, 130])
+def test_small_batch_routing_at_256(dev, N):
+    """gd_set_fused_min_batch (96): 256^2 Gaussian batches below it run the chained kernels (init and iterations),
+    bit for bit the gd_set_fused_iteration(0) / gd_set_fused_init(0) forward; from it on the whole-galaxy kernels,
+    bit for bit the forced-fused forward.  Either way within rounding of the other and of the oracle."""
+    from gdeconv import _lib
+    from gdeconv.synth import make_batch
+    lib = _lib.load()
+    n = 3
+    obs, psf, alpha, _ = make_batch(N, 256, seed=600 + N, device=dev)
+    gen = torch.Generator().manual_seed(N)
+    rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
+    m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
+    assert lib.gd_set_fused_min_batch(-1) == 96
+    with torch.no_grad():
+        default = m(obs, psf, alpha).cpu()
+        with _whole_galaxy_kernels_at_any_batch():
+            fused = m(obs, psf, alpha).cpu()
+        old, old_i = lib.gd_set_fused_iteration(0), lib.gd_set_fused_init(0)
+        try:
+            chained = m(obs, psf, alpha).cpu()
+        finally:
+            lib.gd_set_fused_iteration(old)
+            lib.gd_set_fused_init(old_i)
+    assert torch.equal(default, chained if N < 96 else fused)
+    assert nerr(fused, chained) < 5e-6
+    idx = [0, N - 1]
+    ref = O.admm_forward(obs[idx].cpu(), psf[idx].cpu(), alpha[idx].cpu(), rho1[idx].cpu(), rho2[idx].cpu())
+    assert nerr(default[idx], ref) < TOL
 
 
 @pytest.mark.parametrize("L", [32, 48, 64, 96, 128])
@@ -741,7 +789,8 @@ def test_fused_init_matches_chunked_chain(dev, h, variant, N):
             lib.gd_set_fused_init(on)
             st = engine.ADMMState(obs, psf, alpha, "Gaussian")
             st.state.fill_(0)
-            st.init((r2, 1))
+            with _whole_galaxy_kernels_at_any_batch():
+                st.init((r2, 1))
             torch.cuda.synchronize()
             outs.append([t.clone().cpu() for t in (*_gauss_state_parts(st), st.zin)])
     finally:
@@ -764,7 +813,7 @@ def test_admm256_fused_init_end_to_end(dev, fused_init):
     m = _spectral_model(8, "Gaussian", dev, T(g["Gaussian_rho1"]), T(g["Gaussian_rho2"]))
     old = lib.gd_set_fused_init(fused_init)
     try:
-        with torch.no_grad():
+        with torch.no_grad(), _whole_galaxy_kernels_at_any_batch():
             out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
     finally:
         lib.gd_set_fused_init(old)
