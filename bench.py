@@ -439,12 +439,13 @@ def measure(args, ctx):
     mid_fused = bool(fused) and args.size in (80, 96, 112, 128, 144, 160) and args.llh == "Gaussian"
     # 256^2 Gaussian batches below gd_set_fused_min_batch run the chained kernels (one-workgroup-per-galaxy launches
     # of fewer than ~a round of workgroups leave most CUs idle)
-    min_batch = lib.gd_set_fused_min_batch(-1)
+    min_batch = lib.gd_set_fused_min_batch(0, -1)
     small_chained = args.size == 256 and args.llh == "Gaussian" and args.batch < min_batch
     use_fused = bool(fused) and (not generic or mid_fused) and args.llh == "Gaussian" and not small_chained
     if small_chained:
         fused_init = 0
-    pois2 = bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
+    pois2 = (bool(fused) and args.size == 256 and args.llh == "Poisson"  # two whole-galaxy passes per iteration
+             and args.batch >= lib.gd_set_fused_min_batch(1, -1))
     # Poisson at L <= 112: one workgroup per galaxy, both images in LDS (k_pois_small, k_pois_small_init)
     pois_small = bool(fused) and args.llh == "Poisson" and args.size in (32, 48, 64, 80, 96, 112)
     if args.pipe_streams is not None:
@@ -463,6 +464,7 @@ def measure(args, ctx):
         use_fused = False
         fused_rl = lib.gd_set_fused_rl(1)
         lib.gd_set_fused_rl(fused_rl)
+        fused_rl = fused_rl and N >= lib.gd_set_fused_min_batch(2, -1)   # small batches: the chunked chain
         rl_impl = ("fused, k_rl_reg (OTF, then each galaxy's whole loop in one 512-thread workgroup; x, y, OTF "
                    "re-read from the Infinity Cache)" if (fused_rl and L == 256) else
                    "whole RL loop per Infinity-Cache chunk (RIF/C chain)")

@@ -2326,6 +2326,11 @@ int g_fused_init = 1;  // Gaussian init (256^2: k_psf_rows<STATE> + k_gal_reg_in
 // N < 256 leaves idle (r06j: N = 1 2.1x, 8 2.1x, 32 1.62x, 64 1.28x faster chained; 128 1.17x, 256 1.82x faster fused).
 // The Gaussian state layout is the same either way, so the choice is per call.
 int g_fused_min_n = 96;
+// the same for the Poisson two-pass at 256^2 (the state layout follows: 2 from this batch up, 3 below; r06k: the
+// three-kernel chain 3.6x at N = 1, 1.86x at 64, 1.17x at 128 faster, the two-pass 1.25x at 256) and for k_rl_reg
+// (the chunked chain 2.6x at N = 1, 1.46x at 64 faster; k_rl_reg 1.05x at 128, 2.0x at 256)
+int g_pois2_min_n = 192;
+int g_rl_min_n = 96;
 
 // Eager pipelined operations fork onto the device's internal streams (PipeRes, shared by the host threads, one
 // operation at a time under its mutex).  Under stream capture (mode 2, gd_set_capture_pipeline) an operation
@@ -2699,7 +2704,7 @@ struct Ops {
     }
     static int richardson_lucy(Args a0, int n_iters, hipStream_t st0) {
         if constexpr (has_fused<L>()) {
-            if (g_fused_rl && n_iters > 0) {
+            if (g_fused_rl && n_iters > 0 && a0.N >= g_rl_min_n) {
                 // the OTF (chunked psf_to_otf), then every galaxy's whole loop in one launch
                 GD_TRY(for_chunks(a0, L, st0, [&](const Args& a, hipStream_t st) { return psf_to_otf(a, st); }));
                 return Lc::rl_reg(a0, n_iters, st0);
@@ -2938,14 +2943,16 @@ size_t gd_admm_state_bytes(int N, int H, int W, int llh) {
 }
 
 namespace {
-bool pois_two_pass(int H, int W, int llh) { return llh == GD_LLH_POISSON && H == 256 && W == 256 && g_fused != 0; }
+bool pois_two_pass(int N, int H, int W, int llh) {
+    return llh == GD_LLH_POISSON && H == 256 && W == 256 && g_fused != 0 && N >= g_pois2_min_n;
+}
 // state layout - Gaussian: [|H|^2 (fp32) | conj(H)F(y/alpha) | F(u1) | conj(H)F(v-u2)] (spectral; at 256^2 with
 // kStateSlotGap bytes between the slots);
 // Poisson: [otf | u1 | w]
 void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
     const size_t spec = (size_t)N * (W / 2 + 1) * H;
     float2* base = reinterpret_cast<float2*>(state);
-    if (pois_two_pass(H, W, llh)) {
+    if (pois_two_pass(N, H, W, llh)) {
         a.s_hh = reinterpret_cast<float*>(base);
         float2* c = base + spec / 2;
         a.s_g = c;                 // the OTF H
@@ -2971,11 +2978,12 @@ void bind_state(Args& a, void* state, int N, int H, int W, int llh) {
 }
 }  // namespace
 
-int gd_admm_state_layout(int H, int W, int llh) {
+int gd_admm_state_layout(int N, int H, int W, int llh) {
     if (!gd_supported_size(H, W)) return GD_ERR_UNSUPPORTED;
+    if (N < 0) return GD_ERR_ARG;
     if (llh == GD_LLH_GAUSSIAN) return 1;
     if (llh != GD_LLH_POISSON) return GD_ERR_ARG;
-    return pois_two_pass(H, W, llh) ? 2 : (pois_split(H, W) ? 4 : 3);
+    return pois_two_pass(N, H, W, llh) ? 2 : (pois_split(H, W) ? 4 : 3);
 }
 
 int gd_admm_init_reads_rho(int H, int W, int llh) {
@@ -3004,7 +3012,7 @@ int gd_admm_init(const float* y, const float* psf, long long psf_gstride, int h,
     ProfScope ps("op_admm_init<" + std::to_string(H) + "," + std::to_string(llh) + ">", (hipStream_t)stream, 1);
     if (llh == GD_LLH_GAUSSIAN)
         return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_init_gauss(a, (hipStream_t)stream); });
-    if (pois_two_pass(H, W, llh)) return Ops<256>::admm_init_pois2(a, (hipStream_t)stream);
+    if (pois_two_pass(N, H, W, llh)) return Ops<256>::admm_init_pois2(a, (hipStream_t)stream);
     return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_init(a, (hipStream_t)stream); });
 }
 
@@ -3036,7 +3044,7 @@ int gd_admm_iter(const float* y, const float* z, float* zin_or_out, const float*
         a.o0 = zin_or_out;
         return dispatch<Ops>(H, W, [&](auto op) { return decltype(op)::admm_iter_gauss(a, (hipStream_t)stream); });
     }
-    if (pois_two_pass(H, W, llh)) {
+    if (pois_two_pass(N, H, W, llh)) {
         a.a0 = z;
         a.o0 = zin_or_out;
         return Ops<256>::admm_iter_pois2(a, (hipStream_t)stream);
@@ -3267,9 +3275,11 @@ int gd_set_fused_rl(int on) {
     return old;
 }
 
-int gd_set_fused_min_batch(int n) {
-    const int old = g_fused_min_n;
-    if (n >= 0) g_fused_min_n = n;
+int gd_set_fused_min_batch(int op, int n) {
+    int* t = op == GD_LLH_GAUSSIAN ? &g_fused_min_n : op == GD_LLH_POISSON ? &g_pois2_min_n : op == 2 ? &g_rl_min_n : nullptr;
+    if (!t) return fail(GD_ERR_ARG, "gd_set_fused_min_batch: op must be 0 (Gaussian), 1 (Poisson) or 2 (Richardson-Lucy)");
+    const int old = *t;
+    if (n >= 0) *t = n;
     return old;
 }
 

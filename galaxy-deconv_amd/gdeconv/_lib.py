@@ -36,7 +36,7 @@ SIGNATURES = {
     "gd_rfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_irfft2": (_I, [_P, _P, _I, _I, _I, _P]),
     "gd_admm_state_bytes": (_SZ, [_I, _I, _I, _I]),
-    "gd_admm_state_layout": (_I, [_I, _I, _I]),
+    "gd_admm_state_layout": (_I, [_I, _I, _I, _I]),
     "gd_admm_init_reads_rho": (_I, [_I, _I, _I]),
     "gd_admm_init": (_I, [_P, _P, _LL, _I, _I, _P, _LL, _P, _LL, _I, _I, _I, _I, _P, _P, _P, _P]),
     "gd_admm_iter": (_I, [_P, _P, _P, _P, _LL, _P, _LL, _P, _LL, _P, _LL, _I, _I, _I, _I, _I, _I, _P, _P,
@@ -59,7 +59,7 @@ SIGNATURES = {
     "gd_set_fused_rl": (_I, [_I]),
     "gd_set_subnet_fused_max": (_I, [_I]),
     "gd_set_fused_init": (_I, [_I]),
-    "gd_set_fused_min_batch": (_I, [_I]),
+    "gd_set_fused_min_batch": (_I, [_I, _I]),
     "gd_subnet_param_count": (_I, []),
     "gd_subnet_features": (_I, [_P, _P, _P, _I, _P]),
     "gd_subnet_mlp_param_count": (_I, [_I]),

@@ -612,7 +612,7 @@ class ADMMState:
             _lib.check(self.lib.gd_admm_init(
                 yp, k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], ap, as_, r2, r2s, self.llh, self.N, self.H,
                 self.W, sp, self.zin.data_ptr(), wp, _stream(self.dev)), "gd_admm_init")
-        self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
+        self.layout = self.lib.gd_admm_state_layout(self.N, self.H, self.W, self.llh)
         self.iter = 0
 
     def init_with_subnet(self, params, mlp_params, n_out):
@@ -638,7 +638,7 @@ class ADMMState:
                 yp, k.data_ptr(), self.psf_gs, k.shape[2], k.shape[3], ap, as_, self.llh, self.N, self.H, self.W, sp,
                 self.zin.data_ptr(), params.contiguous().data_ptr(), mlp_params.contiguous().data_ptr(),
                 rhos.data_ptr(), int(n_out), wp, _stream(self.dev)), "gd_admm_init_subnet")
-        self.layout = self.lib.gd_admm_state_layout(self.H, self.W, self.llh)
+        self.layout = self.lib.gd_admm_state_layout(self.N, self.H, self.W, self.llh)
         self.iter = 0
         return rhos
 
@@ -714,7 +714,7 @@ class ADMMState:
             dst = out
         else:
             dst = self.zin
-        if self.llh != 0 and self.lib.gd_admm_state_layout(self.H, self.W, self.llh) != self.layout:
+        if self.llh != 0 and self.lib.gd_admm_state_layout(self.N, self.H, self.W, self.llh) != self.layout:
             raise _lib.EngineError("the ADMM state layout changed since init (gd_set_fused_iteration toggled "
                                    "between gd_admm_init and gd_admm_iter)")
         v = self._argv

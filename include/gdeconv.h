@@ -108,10 +108,10 @@ size_t gd_admm_state_bytes(int N, int H, int W, int llh);
  * in two whole-galaxy passes (256^2 with a fused iteration: [|H|^2 | H | U1 | W~ | X] + w), 3 = Poisson
  * three-kernel ([otf | u1 | w]), 4 = Poisson at square L <= 112 with the fused init and iteration (the
  * buffers of 3; the init leaves H x0 in the w slot and reads no rho, iteration 0 forms w1 with its rho2);
- * negative = unsupported.  The Poisson layout follows gd_set_fused_iteration / gd_set_fused_init, so a
- * caller records it at init and checks it before each gd_admm_iter (a toggle in between would bind a
- * different layout than the init wrote). */
-int gd_admm_state_layout(int H, int W, int llh);
+ * negative = unsupported.  The Poisson layout follows gd_set_fused_iteration / gd_set_fused_init and, at 256^2,
+ * the batch (gd_set_fused_min_batch), so a caller records it at init and checks it before each gd_admm_iter (a
+ * toggle in between would bind a different layout than the init wrote). */
+int gd_admm_state_layout(int N, int H, int W, int llh);
 /* 1 if gd_admm_init reads its rho2 argument for (H, W, llh) (Poisson layouts 2 and 3: the first V step
  * is taken in the init), 0 if it does not (Gaussian, every size; Poisson layout 4), negative = unsupported. */
 int gd_admm_init_reads_rho(int H, int W, int llh);
@@ -256,11 +256,14 @@ int gd_set_fused_rl(int on);
  * previous value. */
 int gd_set_subnet_fused_max(int n);
 
-/* 256^2 Gaussian: batches of at least n galaxies run the whole-galaxy kernels (k_gal_reg, the one-launch init) when
- * those are on; smaller batches run the chained row / column kernels, whose many small workgroups fill the CUs that
- * one workgroup per galaxy leaves idle below a round of workgroups (the same state layout: chosen per call, results
- * within rounding).  Default 96; n < 0 only queries.  Returns the previous value; process-wide. */
-int gd_set_fused_min_batch(int n);
+/* 256^2: batches of at least n galaxies run the whole-galaxy kernels when those are on, smaller batches the chained
+ * row / column kernels, whose many small workgroups fill the CUs that one workgroup per galaxy leaves idle below a
+ * round of workgroups (results within rounding of each other).  op 0 = Gaussian ADMM (k_gal_reg and the one-launch
+ * init; the same state layout either way, so chosen per call; default 96), 1 = Poisson ADMM (the two-pass path,
+ * state layout 2, against the three-kernel chain, layout 3: see gd_admm_state_layout; default 192), 2 =
+ * Richardson-Lucy (k_rl_reg against the chunked chain; default 96).  n < 0 only queries.  Returns the previous
+ * value (GD_ERR_ARG for another op); process-wide. */
+int gd_set_fused_min_batch(int op, int n);
 
 /* Fused Gaussian init (replaces the chunked RF_YA -> psf_rows -> C_G_INIT -> RIF_CLAMP -> C_G_W1 chain
  * behind gd_admm_init, models/Unrolled_ADMM.py:170-175 + the first V step :335-336): at 256^2 (PSF side

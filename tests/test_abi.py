@@ -75,7 +75,12 @@ def test_switch_setters_are_strict(lib):
         assert cur in (0, 1)
         assert f(2) == -1 and f(3) == -1 and f(-5) == -1
         assert f(cur) == 1, name              # still 1 after the refused values
-    assert lib.gd_set_fused_min_batch(-1) == 96     # 256^2 Gaussian: chained kernels below one round's worth
+    # 256^2: the chained kernels below these batches (Gaussian, Poisson, Richardson-Lucy); another op is an error
+    assert [lib.gd_set_fused_min_batch(op, -1) for op in (0, 1, 2)] == [96, 192, 96]
+    assert lib.gd_set_fused_min_batch(3, -1) == -1
+    # the Poisson state layout at 256^2 follows the batch: two-pass (2) from 192 galaxies, three-kernel (3) below
+    assert lib.gd_admm_state_layout(4096, 256, 256, 1) == 2 and lib.gd_admm_state_layout(64, 256, 256, 1) == 3
+    assert lib.gd_admm_state_layout(64, 256, 256, 0) == 1 and lib.gd_admm_state_layout(1, 48, 48, 1) == 4
     assert lib.gd_set_capture_pipeline(1) == -2
     prev = lib.gd_set_capture_pipeline(2)
     assert prev in (-1, 0, 2)

@@ -27,6 +27,20 @@ def nerr(out, ref):
     return float(O.normwise_error(out, ref).max())
 
 
+@contextlib.contextmanager
+def _whole_galaxy_kernels_at_any_batch():
+    """256^2 routes batches below gd_set_fused_min_batch (Gaussian 96, Poisson 192, Richardson-Lucy 96) to the chained
+    kernels; tests that exercise the whole-galaxy kernels on small batches lift those thresholds."""
+    from gdeconv import _lib
+    lib = _lib.load()
+    old = [lib.gd_set_fused_min_batch(op, 0) for op in (0, 1, 2)]
+    try:
+        yield
+    finally:
+        for op, v in zip((0, 1, 2), old):
+            lib.gd_set_fused_min_batch(op, v)
+
+
 def report(tag, out, ref):
     """Normwise error (the gate) and the per-pixel error with a 1e-5 max|ref| floor,
     printed and, with GD_PARITY_LOG set, appended to that JSON-lines file; returns the normwise one."""
@@ -115,11 +129,15 @@ def test_richardson_lucy(eng, dev, tag, n):
     g = golden("wiener_rl.npz")
     o, p = T(g["obs" + tag]).to(dev), T(g["psf" + tag]).to(dev)
     from models.Richard_Lucy import Richard_Lucy
-    out = Richard_Lucy(n)(o, p).cpu()
+    ref64 = O.richardson_lucy(o.cpu().double(), p.cpu().double(), n)
+    out = Richard_Lucy(n)(o, p).cpu()   # (at 256^2 one galaxy runs the chunked chain: gd_set_fused_min_batch)
     report(f"Richard_Lucy({n}) {tag}^2 (configs[4] at n=100, 256^2)", out, T(g[f"rl{n}_{tag}"]))
     # RL(100) is ill-conditioned (the reference sits ~3e-6 from fp64): engine-limited gate
-    parity_gate(f"Richard_Lucy({n}) {tag}^2", out, T(g[f"rl{n}_{tag}"]),
-                O.richardson_lucy(o.cpu().double(), p.cpu().double(), n))
+    parity_gate(f"Richard_Lucy({n}) {tag}^2", out, T(g[f"rl{n}_{tag}"]), ref64)
+    if tag == "256":                    # and k_rl_reg, configs[4]'s kernel, on the same galaxy
+        with _whole_galaxy_kernels_at_any_batch():
+            out_reg = Richard_Lucy(n)(o, p).cpu()
+        parity_gate(f"Richard_Lucy({n}) {tag}^2 k_rl_reg", out_reg, T(g[f"rl{n}_{tag}"]), ref64)
 
 
 @pytest.mark.parametrize("n", [1, 10])
@@ -140,7 +158,8 @@ def test_richardson_lucy_fused_matches_chunked(eng, dev, n, shared_psf):
     try:
         for on in (1, 0):
             lib.gd_set_fused_rl(on)
-            outs.append(eng.richardson_lucy(obs, psf, n).cpu())
+            with _whole_galaxy_kernels_at_any_batch():
+                outs.append(eng.richardson_lucy(obs, psf, n).cpu())
     finally:
         lib.gd_set_fused_rl(old)
     fused, chunked = outs
@@ -167,19 +186,6 @@ def _spectral_model(n, llh, dev, rho1, rho2):
     m.Z = torch.nn.Identity()
     m.rhos = lambda k, a: (rho1.to(dev), rho2.to(dev))
     return m
-
-
-@contextlib.contextmanager
-def _whole_galaxy_kernels_at_any_batch():
-    """256^2 routes batches below gd_set_fused_min_batch (96) to the chained kernels; tests that exercise the
-    whole-galaxy kernels on small batches lift that threshold."""
-    from gdeconv import _lib
-    lib = _lib.load()
-    old = lib.gd_set_fused_min_batch(0)
-    try:
-        yield
-    finally:
-        lib.gd_set_fused_min_batch(old)
 
 
 @pytest.fixture(params=[1, 0], ids=["fused_reg", "three_kernel"])
@@ -223,7 +229,7 @@ def test_poisson_two_pass_matches_three_kernel_path(dev, n, fused_init):
     m = _spectral_model(n, "Poisson", dev, rho1, rho2)
     old, old_init = lib.gd_set_fused_iteration(1), lib.gd_set_fused_init(fused_init)
     try:
-        with torch.no_grad():
+        with torch.no_grad(), _whole_galaxy_kernels_at_any_batch():
             out_f = m(obs, psf, alpha).cpu()
             lib.gd_set_fused_iteration(0)
             out_t = m(obs, psf, alpha).cpu()
@@ -281,7 +287,7 @@ def test_small_batch_routing_at_256(dev, N):
     rho1 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
     rho2 = (0.5 + torch.rand(N, 1, 1, n, generator=gen)).to(dev)
     m = _spectral_model(n, "Gaussian", dev, rho1, rho2)
-    assert lib.gd_set_fused_min_batch(-1) == 96
+    assert lib.gd_set_fused_min_batch(0, -1) == 96
     with torch.no_grad():
         default = m(obs, psf, alpha).cpu()
         with _whole_galaxy_kernels_at_any_batch():
@@ -484,7 +490,7 @@ def test_init_overlap_bit_identical(dev, monkeypatch, L, N, llh):
     G = _lib.GD_LLH[llh]
     assert lib.gd_admm_init_reads_rho(L, L, _lib.GD_LLH["Gaussian"]) == 0
     assert lib.gd_admm_init_reads_rho(L, L, _lib.GD_LLH["Poisson"]) == (0 if L <= 112 else 1)
-    assert lib.gd_admm_state_layout(L, L, _lib.GD_LLH["Poisson"]) == (4 if L <= 112 else 2)
+    assert lib.gd_admm_state_layout(N, L, L, _lib.GD_LLH["Poisson"]) == (4 if L <= 112 else 2 if N >= 192 else 3)
     h = min(48, L)
     assert lib.gd_admm_init_subnet_supported(N, L, L, h, h, G, 8) == (1 if L <= 64 else 0)
     obs, psf, alpha, _ = make_batch(N, L, h=h, seed=515 + L, device=dev)
