@@ -10,7 +10,11 @@
 //   I2  per half: row IFFT -> num; x = x * num / div -> out; row FFT -> registers (not after the last)
 // The galaxy's spectra never leave the CU; per iteration it reads y, x and H twice (MALL-resident for
 // the galaxies in flight) and writes x.  Arithmetic per bin / pixel as k_col<C_CONV / C_CONVC> and
-// k_row_invfwd<RIF_RL_RATIO / RIF_RL_UPDATE> (IEEE divisions kept: RL(100) compounds every rounding).
+// k_row_invfwd<RIF_RL_RATIO / RIF_RL_UPDATE>, except the ratio's division (rl_div: a reciprocal and one Newton
+// step) and the update's 1 / div (one reciprocal per galaxy).
+// Neither product carries the chain's 1 / L^2: Hx comes out L^2 too large, y / Hx L^2 too small, and the conj(H)
+// pass's missing 1 / L^2 restores num (L^2 = 2^16: power-of-two scalings, no extra rounding; round 6: 2.6 % fewer
+// VALU instructions, time unchanged - profiles/r06o_rl_ab.txt).
 // The OTF (a.otf, [N][K][L], ky contiguous) is computed beforehand (psf_to_otf).
 // Included inside namespace gd by gd_engine.hip (after gd_galreg.hpp).
 
@@ -44,7 +48,6 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
     using RG = RegGeo<L>;
     constexpr int F1 = RG::F1, F2 = RG::F2, KS = RG::KS, SLD = RG::SLD, LINES = RG::LINES, T = RG::THREADS;
     constexpr int RB0 = RG::RB0, RB1 = RG::RB1, K = RG::K;
-    constexpr float inv_n = float(1.0 / double(L * L));
     __shared__ float2 tw[L];
     __shared__ __attribute__((aligned(16))) float2 S[RG::U];
     __shared__ float2 nyq[RG::NP];  // X_p[L/2] of every pair
@@ -117,7 +120,10 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             };
             auto happly = [&](float2 (&C)[F2], const float2 (&h)[F2]) {
 #pragma unroll
-                for (int s = 0; s < F2; ++s) C[s] = cscale(CONJ ? cmulc(C[s], h[s]) : cmul(C[s], h[s]), inv_n);
+                for (int s = 0; s < F2; ++s) {
+                    const c2 c = tc2(C[s]), hh = tc2(h[s]);
+                    C[s] = tf2(pmul_r<CONJ>(c, hh, pmul_t(c, hh)));
+                }
             };
             auto hmul = [&](float2 (&C)[F2], int kx) {
                 float2 h[F2];
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
 #else
                 const float2 hn = Hg[(size_t)(L / 2) * L + tt];
 #endif
-                nyqc[tt] = cscale(CONJ ? cmulc(nyqc[tt], hn) : cmul(nyqc[tt], hn), inv_n);
+                nyqc[tt] = CONJ ? cmulc(nyqc[tt], hn) : cmul(nyqc[tt], hn);
             }
             lds_barrier();  // Nyquist products
 #pragma unroll
