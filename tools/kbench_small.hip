@@ -6,6 +6,7 @@
 #include "../galaxy-deconv_amd/csrc/gd_engine.hip"
 
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -89,6 +90,15 @@ static void print_trace(unsigned long long* tr, int N, int nph, const char** nam
 }
 #endif
 
+// FNV-1a over the bits of n device floats: variants that must be bit-identical print the same value
+static unsigned long long fnv_dev(const float* p, size_t n) {
+    std::vector<float> v(n);
+    CK(hipMemcpy(v.data(), p, n * 4, hipMemcpyDeviceToHost));
+    unsigned long long h = 1469598103934665603ull;
+    for (float f : v) { unsigned u; memcpy(&u, &f, 4); h = (h ^ u) * 1099511628211ull; }
+    return h;
+}
+
 int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 256, L = argc > 2 ? atoi(argv[2]) : 48, reps = argc > 3 ? atoi(argv[3]) : 200;
     const int h = L < 48 ? L : 48, n_it = 8;
@@ -161,6 +171,8 @@ int main(int argc, char** argv) {
                                            prm, mlp, rh, n_out, ws, st)); }, reps);
             }
         }
+        CK(hipStreamSynchronize(st));
+        printf("rhos fnv %016llx  init zin fnv %016llx\n", fnv_dev(rh, (size_t)N * n_out), fnv_dev(zin, (size_t)N * L * L));
     }
     timeit("init (back to back)", init, reps);
     timeit("middle iteration (back to back)", [&]() { iter(3); }, reps);
@@ -175,7 +187,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
     double s = 0;
     for (float v : ho) s += v;
-    printf("galaxy 0 output sum %.6e\n", s);
+    printf("galaxy 0 output sum %.6e  output fnv %016llx\n", s, fnv_dev(out, (size_t)N * L * L));
 #if GD_FUSED_TRACE
     const char* names[] = {"twiddles + state prefetch", "R: row FFTs", "C: columns + update", "I: inverse rows + store"};
     CK(hipMemset(tr, 0, (size_t)N * 16 * 8));
