@@ -575,7 +575,7 @@ class ADMMState:
         self._bind()
         self.layout = None
         self.iter = 0
-        self._side = None   # the side stream an init_concurrent() is running on, until joined
+        self._side = None   # the _side_streams entry an init_concurrent() is running on, until joined
         # not cached: for Poisson it follows the fused-path switches (state layout 4: iteration 0 forms w1);
         # _reads_rho holds overrides only (tests force the serial order with it)
         r = ADMMState._reads_rho.get((self.H, self.W, self.llh))
@@ -585,7 +585,11 @@ class ADMMState:
 
     _reads_rho = {}     # (H, W, llh) -> forced gd_admm_init_reads_rho (overrides for tests; empty by default)
     _state_bytes = {}   # (N, H, W, llh) -> gd_admm_state_bytes (pure in its arguments)
-    _side_streams = {}  # (device index, main stream) -> the side stream init_concurrent forks onto (LRU, bounded)
+    # (device index, main stream) -> (side stream, fork event, join event) of init_concurrent (LRU, bounded).  The fork
+    # and join go through these persistent events, not Stream.wait_stream's temporary ones: an event recorded during
+    # a capture on the side stream (which itself forks the engine's capture streams) and destroyed before
+    # hipStreamEndCapture is what crashed the ROCm 7 runtime there (tools/capture_probe.hip mode 11)
+    _side_streams = {}
     _SIDE_STREAMS_MAX = 16
 
     @property
@@ -654,13 +658,15 @@ class ADMMState:
         # do not serialise their inits on a shared side stream (nor join each other's); a bounded cache, so
         # the streams of callers that come and go are not kept forever
         key = (self._dev_index, main.cuda_stream)
-        side = ADMMState._side_streams.pop(key, None)
-        if side is None:
-            side = torch.cuda.Stream(device=self.dev)
-        ADMMState._side_streams[key] = side          # most recently used last
+        entry = ADMMState._side_streams.pop(key, None)
+        if entry is None:
+            entry = (torch.cuda.Stream(device=self.dev), torch.cuda.Event(), torch.cuda.Event())
+        ADMMState._side_streams[key] = entry         # most recently used last
         while len(ADMMState._side_streams) > ADMMState._SIDE_STREAMS_MAX:
             ADMMState._side_streams.pop(next(iter(ADMMState._side_streams)))
-        side.wait_stream(main)
+        side, fork, _ = entry
+        fork.record(main)
+        side.wait_event(fork)
         # under stream capture a chunked init on the side stream runs its chunks in sequence: a fork from a
         # stream that joined the capture through an event onto the library's pipeline streams crashed the ROCm 7
         # runtime inside hipStreamEndCapture (gd_set_capture_pipeline)
@@ -672,12 +678,14 @@ class ADMMState:
         finally:
             if capturing:
                 self.lib.gd_set_capture_pipeline(old)
-        self._side = side
+        self._side = entry
 
     def join(self):
         """Make the device's current stream wait for an ``init_concurrent`` (no-op otherwise)."""
         if self._side is not None:
-            torch.cuda.current_stream(self.dev).wait_stream(self._side)
+            side, _, ev = self._side
+            ev.record(side)
+            torch.cuda.current_stream(self.dev).wait_event(ev)
             self._side = None
 
     def _bind(self):

@@ -6,6 +6,14 @@
 //   mode 2: mode 0's fork / join on a stream B that joined the capture through an event (ADMMState.init_concurrent's
 //           side stream), B joined back at the end; mode 3: the same with kernels on the capturing stream meanwhile;
 //   mode 6: mode 2 with the A -> B event destroyed right after B's wait (what torch's Stream.wait_stream does)
+//   mode 7: mode 2's K fork / joins on B, B joined back to A, then K more on A itself onto the SAME internal streams
+//           (the engine under capture: the init's chunks forked from the side stream, the iterations' from the
+//           capturing stream, one set of capture streams); mode 8: the same in the opposite order (A first, then B)
+//   mode 9: mode 7 with the internal streams CREATED after hipStreamBeginCapture (the engine's capture streams are
+//           created at a thread's first pipelined operation under capture), so their first capture join is through
+//           B; mode 10: the same creation with the first fork from A (mode 8's order)
+//   mode 11: mode 2 with B joined back to A through a temporary event destroyed right after A's wait (torch's
+//           Stream.wait_stream at ADMMState.join: the event was recorded on B, a stream that has forked streams)
 // Then hipStreamEndCapture, instantiate, launch twice, and check the result on the host.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/bin/capture_probe tools/capture_probe.hip
 //   tools/bin/capture_probe MODE K M [S=2] [KPC=3]
@@ -29,8 +37,12 @@ int main(int argc, char** argv) {
     CK(hipMemset(buf, 0, (size_t)M * n * 4));
     hipStream_t st, side[8];
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    for (int i = 0; i < S; ++i) CK(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
-    const int sets = mode == 1 ? K : 1;
+    const bool late = mode == 9 || mode == 10;
+    if (!late)
+        for (int i = 0; i < S; ++i) CK(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
+    // PROBE_FRESH=1: modes >= 2 take a fresh event set per fork / join as well (the engine's ring of kCapSets sets)
+    const bool fresh = mode == 1 || (std::getenv("PROBE_FRESH") && std::atoi(std::getenv("PROBE_FRESH")) == 1);
+    const int sets = fresh ? 2 * K : 1;
     std::vector<hipEvent_t> fork(sets), join((size_t)sets * S);
     for (auto& e : fork) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : join) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -60,6 +72,8 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
     if (mode == 4) CK(hipStreamCreateWithFlags(&B, hipStreamNonBlocking));
+    if (late)
+        for (int i = 0; i < S; ++i) CK(hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking));
     hipStream_t cap = st;
     if (mode >= 2) {
         CK(hipEventRecord(eAB, st));
@@ -67,8 +81,20 @@ int main(int argc, char** argv) {
         if (mode == 6) CK(hipEventDestroy(eAB));  // torch's Stream.wait_stream: a temporary event, destroyed at once
         cap = B;
     }
-    for (int k = 0; k < K; ++k) {
-        const int e = mode == 1 ? k : 0;
+    const bool mixed = mode == 7 || mode == 8 || late;
+    const bool a_first = mode == 8 || mode == 10;
+    if (a_first) cap = st;
+    for (int k = 0; k < (mixed ? 2 * K : K); ++k) {
+        const int e = fresh ? k : 0;
+        if (mixed && k == K) {  // switch the forking stream: B -> A (mode 7) or A -> B (mode 8)
+            if (!a_first) {
+                CK(hipEventRecord(eBA, B));
+                CK(hipStreamWaitEvent(st, eBA, 0));
+                cap = st;
+            } else {
+                cap = B;
+            }
+        }
         hipStream_t st = cap;
         CK(hipEventRecord(fork[e], st));
         for (int i = 0; i < S; ++i) CK(hipStreamWaitEvent(side[i], fork[e], 0));
@@ -80,17 +106,46 @@ int main(int argc, char** argv) {
             CK(hipStreamWaitEvent(st, join[(size_t)e * S + i], 0));
         }
     }
-    if (mode >= 2) {
+    if (mode >= 2 && !(mixed && !a_first)) {
         if (mode == 3)
             for (int j = 0; j < KPC; ++j) hipLaunchKernelGGL(k_add, dim3(n / 256), dim3(256), 0, st, buf, n, 0.0f);
-        CK(hipEventRecord(eBA, B));
-        CK(hipStreamWaitEvent(st, eBA, 0));
+        if (mode == 11) {
+            hipEvent_t tmp;
+            CK(hipEventCreateWithFlags(&tmp, hipEventDisableTiming));
+            CK(hipEventRecord(tmp, B));
+            CK(hipStreamWaitEvent(st, tmp, 0));
+            CK(hipEventDestroy(tmp));
+        } else {
+            CK(hipEventRecord(eBA, B));
+            CK(hipStreamWaitEvent(st, eBA, 0));
+        }
     }
-    printf("mode %d (%s) K=%d M=%d S=%d: captured, ending capture\n", mode,
+    printf("mode %d%s (%s) K=%d M=%d S=%d: captured, ending capture\n", mode, fresh && mode != 1 ? " fresh" : "",
            mode == 0 ? "shared events" : mode == 1 ? "fresh events" : mode == 2 ? "nested via stream B" :
            mode == 3 ? "nested + work on A" : mode == 4 ? "nested, B created during the capture" :
-           mode == 5 ? "nested, streams used eagerly first" : "nested, the A->B event destroyed right after B's wait",
+           mode == 5 ? "nested, streams used eagerly first" : mode == 6 ? "nested, the A->B event destroyed right after B's wait" :
+           mode == 7 ? "internal streams forked from B, then from A" : mode == 8 ? "internal streams forked from A, then from B" :
+           mode == 9 ? "internal streams created in the capture, forked from B, then A" : mode == 10 ? "internal streams created in the capture, forked from A, then B" :
+                        "nested, B joined to A by a temporary event destroyed after the wait",
            K, M, S);
+    // every stream's capture state just before hipStreamEndCapture: status (0 none, 1 active, 2 invalidated), capture
+    // id and the number of nodes its next captured operation would depend on (its unjoined tail)
+    auto info = [&](const char* name, hipStream_t x) {
+        hipStreamCaptureStatus cs;
+        unsigned long long id = 0;
+        hipGraph_t gg = nullptr;
+        const hipGraphNode_t* deps = nullptr;
+        size_t nd = 0;
+        const hipError_t e = hipStreamGetCaptureInfo_v2(x, &cs, &id, &gg, &deps, &nd);
+        printf("  %-8s err %d status %d id %llu graph %p deps %zu\n", name, (int)e, (int)cs, id, (void*)gg, nd);
+    };
+    info("A", st);
+    if (B) info("B", B);
+    for (int i = 0; i < S; ++i) {
+        char nm[16];
+        snprintf(nm, sizeof nm, "int%d", i);
+        info(nm, side[i]);
+    }
     fflush(stdout);
     hipGraph_t g;
     CK(hipStreamEndCapture(st, &g));
@@ -105,7 +160,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(st));
     std::vector<float> h((size_t)M * n);
     CK(hipMemcpy(h.data(), buf, h.size() * 4, hipMemcpyDeviceToHost));
-    const float want = 2.0f * K * KPC;
+    const float want = 2.0f * K * KPC * (mixed ? 2 : 1);
     long bad = 0;
     for (float v : h) bad += (v != want);
     printf("  replayed twice: %s (expected %.0f per element, %ld wrong)\n", bad ? "WRONG" : "ok", want, bad);
