@@ -2862,6 +2862,12 @@ const char* gd_engine_rev(void) { return "r06.1"; }
 static const char g_src_hash_marker[] = "gdsrc:" GD_SRC_HASH;
 const char* gd_engine_src_hash(void) { return g_src_hash_marker + 6; }
 
+int gd_hip_runtime_version(void) {
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return fail(GD_ERR_HIP, "hipRuntimeGetVersion");
+    return v;
+}
+
 const char* gd_last_error(void) { return g_last_error.c_str(); }
 
 int gd_supported_size(int H, int W) {

@@ -26,6 +26,7 @@ SIGNATURES = {
     "gd_abi_version": (_I, []),
     "gd_engine_rev": (ctypes.c_char_p, []),
     "gd_engine_src_hash": (ctypes.c_char_p, []),
+    "gd_hip_runtime_version": (_I, []),
     "gd_last_error": (ctypes.c_char_p, []),
     "gd_supported_size": (_I, [_I, _I]),
     "gd_workspace_bytes": (_SZ, [_I, _I, _I]),

@@ -539,6 +539,18 @@ def _scalar_arg(x, dev):
     return int(p), s
 
 
+_NESTED_FORK_SAFE = None
+
+
+def _nested_capture_fork_safe(lib):
+    """True when the HIP runtime this process runs on captures a fork from a non-origin capture stream (ROCm >= 7.2;
+    7.0, which PyTorch 2.10+rocm7.0 bundles, segfaults in hipStreamEndCapture on it)."""
+    global _NESTED_FORK_SAFE
+    if _NESTED_FORK_SAFE is None:
+        _NESTED_FORK_SAFE = lib.gd_hip_runtime_version() >= 70200000
+    return _NESTED_FORK_SAFE
+
+
 class ADMMState:
     """Device state of one unrolled-ADMM forward: the engine's opaque state buffer (OTF + u1 and
     v - u2, spectral for llh='Gaussian', spatial for 'Poisson'), ``zin``, the next denoiser input
@@ -667,16 +679,18 @@ class ADMMState:
         side, fork, _ = entry
         fork.record(main)
         side.wait_event(fork)
-        # under stream capture a chunked init on the side stream runs its chunks in sequence: a fork from a
-        # stream that joined the capture through an event onto the library's pipeline streams crashed the ROCm 7
-        # runtime inside hipStreamEndCapture (gd_set_capture_pipeline)
-        capturing = torch.cuda.is_current_stream_capturing()
-        old = self.lib.gd_set_capture_pipeline(0) if capturing else None
+        # under stream capture a chunked init on the side stream runs its chunks in sequence on HIP runtimes before
+        # 7.2: there a fork from a stream that joined the capture through an event (the side stream) onto other
+        # streams segfaults inside hipStreamEndCapture - a runtime bug, reproduced without the engine by
+        # tools/capture_probe.hip mode 2 on PyTorch's bundled ROCm 7.0 runtime and absent on ROCm 7.2's
+        # (profiles/r06_capture_rootcause.txt)
+        serial = torch.cuda.is_current_stream_capturing() and not _nested_capture_fork_safe(self.lib)
+        old = self.lib.gd_set_capture_pipeline(0) if serial else None
         try:
             with torch.cuda.stream(side):
                 self.init(None)
         finally:
-            if capturing:
+            if serial:
                 self.lib.gd_set_capture_pipeline(old)
         self._side = entry
 

@@ -10,8 +10,9 @@ opts in (``gd_set_capture_pipeline``, per host thread); ``GraphedForward`` opts 
 it enqueues from the capturing stream itself: the chunks then fork onto capture streams of this host thread
 (never the internal streams other threads' eager calls use), a fork / join per operation with its own
 captured event set.  An init that ``ADMMState.init_concurrent`` runs on a side stream keeps its chunks serial
-there: a fork nested inside that side stream's own fork was what crashed the ROCm 7 runtime when the graph
-was instantiated (``profiles/r04dbg_160_graph_crash.txt``, ``profiles/r05b_capture_probe.txt``).
+there on HIP runtimes before 7.2: a fork from a stream that joined the capture through an event segfaults inside
+hipStreamEndCapture on the ROCm 7.0 runtime PyTorch bundles, with or without the engine (``tools/capture_probe.hip``
+mode 2; ROCm 7.2's runtime captures it; ``profiles/r06_capture_rootcause.txt``).
 A mode the caller set with ``gd_set_capture_pipeline`` before constructing is kept.  A server whose other host
 threads keep launching work while one thread captures passes ``capture_error_mode="thread_local"`` (torch's
 default "global" mode invalidates the capture on another thread's potentially unsafe call).

@@ -61,6 +61,9 @@ const char* gd_engine_rev(void);
 /* sha256 prefix (16 hex digits) of the sources this library was compiled from (the csrc .hip and .hpp
    files and this header; __graft_entry__.build passes it in): smoke() compares it with the tree it runs in */
 const char* gd_engine_src_hash(void);
+/* hipRuntimeGetVersion of the HIP runtime this library runs on (in a PyTorch process: the runtime PyTorch bundles,
+   e.g. 70051831 = ROCm 7.0 for torch 2.10+rocm7.0, whatever /opt/rocm holds), or a negative error code */
+int gd_hip_runtime_version(void);
 const char* gd_last_error(void);
 int gd_supported_size(int H, int W);  /* 1 compile-time-planned, 2 runtime-planned, 0 unsupported */
 size_t gd_workspace_bytes(int N, int H, int W);
@@ -229,8 +232,10 @@ int gd_set_pipeline_streams(int streams);
  * operation's chunks in sequence on the capturing stream; mode 2 forks them onto streams of the calling thread (never
  * the internal streams eager calls of other threads use, since streams that join a capture stay in it until
  * hipStreamEndCapture), each operation with an event set of its own.  Opt in to 2 only when enqueuing from the
- * capturing stream itself (gdeconv.graphs.GraphedForward does): a fork from a stream that joined the capture through
- * an event crashed the ROCm 7 runtime inside hipStreamEndCapture.  -1 restores the default (the GD_CAPTURE_PIPELINE
+ * capturing stream itself (gdeconv.graphs.GraphedForward does) when the HIP runtime is older than 7.2
+ * (gd_hip_runtime_version() < 70200000): there a fork from a stream that joined the capture through an event (onto
+ * any other streams, no engine call needed) segfaults inside hipStreamEndCapture; ROCm 7.2's runtime captures the
+ * same sequence (tools/capture_probe.hip mode 2).  -1 restores the default (the GD_CAPTURE_PIPELINE
  * environment variable, 0 or 2, else 0).  Returns the previous override (-1: none), or GD_ERR_UNSUPPORTED (setting
  * unchanged) for any other mode. */
 int gd_set_capture_pipeline(int mode);

@@ -111,7 +111,10 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(A));
     std::vector<float> ref((size_t)N * L * L), got(ref.size());
     CK(hipMemcpy(ref.data(), out, ref.size() * 4, hipMemcpyDeviceToHost));
-    printf("side %d, %d x %d^2, chunk bytes %zu: eager forward done; capturing\n", side, N, L, (N / chunks + 1) * tgal);
+    int rtv = 0;
+    CK(hipRuntimeGetVersion(&rtv));
+    printf("side %d, %d x %d^2, chunk bytes %zu, HIP runtime %d: eager forward done; capturing\n", side, N, L,
+           (N / chunks + 1) * tgal, rtv);
     fflush(stdout);
     CK(hipStreamBeginCapture(A, hipStreamCaptureModeGlobal));
     forward(true);

@@ -32,6 +32,9 @@ int main(int argc, char** argv) {
     const int mode = argc > 1 ? atoi(argv[1]) : 0, K = argc > 2 ? atoi(argv[2]) : 8, M = argc > 3 ? atoi(argv[3]) : 9;
     const int S = argc > 4 ? atoi(argv[4]) : 2, KPC = argc > 5 ? atoi(argv[5]) : 3;
     const int n = 1 << 16;
+    int rtv = 0;
+    CK(hipRuntimeGetVersion(&rtv));
+    printf("HIP runtime %d\n", rtv);
     float* buf;
     CK(hipMalloc(&buf, (size_t)M * n * 4));
     CK(hipMemset(buf, 0, (size_t)M * n * 4));

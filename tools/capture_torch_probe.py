@@ -10,6 +10,8 @@ topology with plain HIP capture and does not crash.
       main     : prealloc with the init on the capturing stream itself (its chunks forked from the origin)
       ext      : prealloc under torch.cuda.graph, the capturing and the side stream created with hipStreamCreateWithFlags
                  (non-blocking) through ctypes and wrapped as torch.cuda.ExternalStream
+      pure     : prealloc; every stream, event and the capture itself through ctypes HIP calls (torch only allocates the
+                 buffers): the C++ probe's call sequence from inside a torch process
       hipcap   : prealloc, captured with hipStreamBeginCapture / hipStreamEndCapture (ctypes) on a torch stream
                  instead of torch.cuda.graph (torch's streams, not torch's CUDAGraph)
 """
@@ -79,6 +81,8 @@ def main():
             assert rc == 0, lib.gd_last_error()
         return out
 
+    if variant == "pure":
+        return pure(lib, hip, N, L, n_it, h, y, psf, alpha, rho1, rho2, state, ws, out, zin_pre)
     with torch.no_grad():
         ref = forward(False).clone()
     torch.cuda.synchronize()
@@ -105,6 +109,45 @@ def main():
         out.zero_()
         g.replay()
     torch.cuda.synchronize()
+    print(f"[torch probe] replay bit-identical to eager: {bool(torch.equal(out, ref))}", flush=True)
+
+
+def pure(lib, hip, N, L, n_it, h, y, psf, alpha, rho1, rho2, state, ws, out, zin):
+    vp = ctypes.c_void_p
+    A, B = vp(), vp()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(A), 1) == 0 and hip.hipStreamCreateWithFlags(ctypes.byref(B), 1) == 0
+    eAB, eBA = vp(), vp()
+    assert hip.hipEventCreateWithFlags(ctypes.byref(eAB), 2) == 0 and hip.hipEventCreateWithFlags(ctypes.byref(eBA), 2) == 0
+
+    def forward():
+        assert hip.hipEventRecord(eAB, A) == 0 and hip.hipStreamWaitEvent(B, eAB, 0) == 0
+        rc = lib.gd_admm_init(y.data_ptr(), psf.data_ptr(), h * h, h, h, alpha.data_ptr(), 1, None, 0, 0, N, L, L,
+                              state.data_ptr(), zin.data_ptr(), ws.data_ptr(), B)
+        assert rc == 0, lib.gd_last_error()
+        assert hip.hipEventRecord(eBA, B) == 0 and hip.hipStreamWaitEvent(A, eBA, 0) == 0
+        for it in range(n_it):
+            last = it == n_it - 1
+            dst = out if last else zin
+            rc = lib.gd_admm_iter(y.data_ptr(), zin.data_ptr(), dst.data_ptr(), alpha.data_ptr(), 1,
+                                  rho1[:, it:].data_ptr(), n_it, rho2[:, it:].data_ptr(), n_it,
+                                  None if last else rho2[:, it + 1:].data_ptr(), n_it, 0, it, int(last), N, L, L,
+                                  state.data_ptr(), ws.data_ptr(), A)
+            assert rc == 0, lib.gd_last_error()
+    torch.cuda.synchronize()
+    forward()
+    assert hip.hipStreamSynchronize(A) == 0
+    ref = out.clone()
+    print("[torch probe] pure: eager done; capturing", flush=True)
+    assert hip.hipStreamBeginCapture(A, 0) == 0
+    forward()
+    graph, ge = vp(), vp()
+    rc = hip.hipStreamEndCapture(A, ctypes.byref(graph))
+    assert rc == 0, rc
+    print("[torch probe] end capture ok", flush=True)
+    assert hip.hipGraphInstantiate(ctypes.byref(ge), graph, None, None, ctypes.c_size_t(0)) == 0
+    out.zero_()
+    torch.cuda.synchronize()
+    assert hip.hipGraphLaunch(ge, A) == 0 and hip.hipStreamSynchronize(A) == 0
     print(f"[torch probe] replay bit-identical to eager: {bool(torch.equal(out, ref))}", flush=True)
 
 
