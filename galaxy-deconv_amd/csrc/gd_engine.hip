@@ -3128,7 +3128,7 @@ int check_gx(int N, int H, int W) {
     // whose crop_half no longer matches the image in the reference); H != W pads each side on its own
     // (a 2H x 2W grid: the runtime-planned path, which sizes the padding per axis)
     if (H % 2 || W % 2 || !gd_supported_size(2 * H, 2 * W) || (specialised_size(2 * H, 2 * W) && H % 4))
-        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: images of even sides 2 .. 818 (2x padded grid)");
+        return fail(GD_ERR_UNSUPPORTED, "UnrolledADMMGaussian: images of even sides 2 .. 2048 (2x padded grid)");
     return GD_OK;
 }
 // half spectrum of the 2H x 2W grid, [N][W + 1][2H] (complex elements)

@@ -1,4 +1,4 @@
-// gd_generic.hpp - the runtime-size path: any H x W image with 2 <= H, W <= 1638, square or not.
+// gd_generic.hpp - the runtime-size path: any H x W image with 2 <= H, W <= 4096, square or not.
 //
 // The specialised sizes (square 32, 48, 64, 96, 128, 256) run the compile-time-planned kernels of
 // gd_engine.hip.  Every other size the reference's torch.fft path accepts (utils/utils_torch.py:22-27,
@@ -17,15 +17,19 @@
 //    row that is never stored; columns are contiguous in the transposed half-spectrum layout
 //    [N][W/2+1][H], so column lines load and store coalesced.
 //
-// Dynamic LDS per workgroup: (n + 2 lines n) float2 <= 64 KiB.
+// Dynamic LDS per workgroup: (n + 2 lines n) float2 <= 64 KiB for lines of n <= 1638 points; longer lines (up to 4096,
+// the gfx950 CU's whole 160 KiB for a two-image workgroup) take the larger budget, one workgroup per CU.
 #pragma once
 
 namespace gen {
 
-constexpr int kMaxLen = 1638;     // per axis: a two-image workgroup (one line each, plus the ping-pong buffers), 5 n float2, in 64 KiB of LDS
+// per axis: a two-image workgroup (one line each, plus the ping-pong buffers) needs 5 n float2 of LDS
+constexpr int kMaxLen = 4096;      // 5 n float2 in the CU's 160 KiB
+constexpr int kSmallLen = 1638;    // 5 n float2 in 64 KiB: the budget of every line up to here (rounds 1-5 unchanged)
 constexpr int kMaxStages = 16;
 constexpr int kThreads = 256;
-constexpr int kLdsFloat2 = 8192;  // 64 KiB
+constexpr int kLdsFloat2 = 8192;   // 64 KiB
+constexpr int kLdsFloat2Big = 20480;  // 160 KiB (gfx950 LDS per CU)
 constexpr int kMaxLines = 16;
 
 struct Axis {
@@ -39,7 +43,7 @@ struct Dims {
 };
 
 __host__ __device__ inline int lines_for(int n) {
-    const int l = (kLdsFloat2 - n) / (2 * n);
+    const int l = ((n <= kSmallLen ? kLdsFloat2 : kLdsFloat2Big) - n) / (2 * n);
     return l < 1 ? 1 : (l > kMaxLines ? kMaxLines : l);
 }
 // row pairs per workgroup per image (NI images), and columns per workgroup (NIC lines per column)
@@ -655,6 +659,13 @@ struct GLaunch {
     static std::string nm(const char* k, int mode, const Dims& d) {
         return std::string(k) + "<" + std::to_string(d.H) + "x" + std::to_string(d.W) + "," + std::to_string(mode) + ">";
     }
+    // dynamic LDS above 64 KiB (lines longer than kSmallLen) must be allowed per kernel before its launch
+    static int allow_lds(const void* k, size_t bytes) {
+        if (bytes <= 65536) return GD_OK;
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+            return fail(GD_ERR_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+        return GD_OK;
+    }
     static int row_grid(int NI, const Args& a, const Dims& d) {
         const int pb = row_pairs(NI, d.W);
         return a.N * (((d.H + 1) / 2 + pb - 1) / pb);
@@ -664,8 +675,9 @@ struct GLaunch {
         const Dims d = dims(a);
         constexpr int NI = RfTraits<MODE>::NI;
         ProfScope ps(nm("k_gen_rf", MODE, d), st);
-        hipLaunchKernelGGL((k_gen_rf<MODE>), dim3(row_grid(NI, a, d)), dim3(kThreads),
-                           lds_bytes(d.W, NI * row_pairs(NI, d.W)), st, a, d);
+        const size_t lb = lds_bytes(d.W, NI * row_pairs(NI, d.W));
+        GD_TRY(allow_lds(reinterpret_cast<const void*>(&k_gen_rf<MODE>), lb));
+        hipLaunchKernelGGL((k_gen_rf<MODE>), dim3(row_grid(NI, a, d)), dim3(kThreads), lb, st, a, d);
         return check_launch("k_gen_rf");
     }
     template <int MODE>
@@ -674,8 +686,9 @@ struct GLaunch {
         constexpr int NIC = GColTraits<MODE>::IN2 ? 2 : 1;
         const int cb = col_cols(NIC, d.H);
         ProfScope ps(nm("k_gen_col", MODE, d), st);
-        hipLaunchKernelGGL((k_gen_col<MODE>), dim3((a.N * d.K + cb - 1) / cb), dim3(kThreads), lds_bytes(d.H, NIC * cb),
-                           st, a, d);
+        const size_t lb = lds_bytes(d.H, NIC * cb);
+        GD_TRY(allow_lds(reinterpret_cast<const void*>(&k_gen_col<MODE>), lb));
+        hipLaunchKernelGGL((k_gen_col<MODE>), dim3((a.N * d.K + cb - 1) / cb), dim3(kThreads), lb, st, a, d);
         return check_launch("k_gen_col");
     }
     template <int MODE>
@@ -683,16 +696,18 @@ struct GLaunch {
         const Dims d = dims(a);
         constexpr int NI = RiTraits<MODE>::NI;
         ProfScope ps(nm("k_gen_ri", MODE, d), st);
-        hipLaunchKernelGGL((k_gen_ri<MODE>), dim3(row_grid(NI, a, d)), dim3(kThreads),
-                           lds_bytes(d.W, NI * row_pairs(NI, d.W)), st, a, d);
+        const size_t lb = lds_bytes(d.W, NI * row_pairs(NI, d.W));
+        GD_TRY(allow_lds(reinterpret_cast<const void*>(&k_gen_ri<MODE>), lb));
+        hipLaunchKernelGGL((k_gen_ri<MODE>), dim3(row_grid(NI, a, d)), dim3(kThreads), lb, st, a, d);
         return check_launch("k_gen_ri");
     }
     template <int MODE>
     static int rif(const Args& a, hipStream_t st) {
         const Dims d = dims(a);
         ProfScope ps(nm("k_gen_rif", MODE, d), st);
-        hipLaunchKernelGGL((k_gen_rif<MODE>), dim3(row_grid(1, a, d)), dim3(kThreads), lds_bytes(d.W, row_pairs(1, d.W)),
-                           st, a, d);
+        const size_t lb = lds_bytes(d.W, row_pairs(1, d.W));
+        GD_TRY(allow_lds(reinterpret_cast<const void*>(&k_gen_rif<MODE>), lb));
+        hipLaunchKernelGGL((k_gen_rif<MODE>), dim3(row_grid(1, a, d)), dim3(kThreads), lb, st, a, d);
         return check_launch("k_gen_rif");
     }
 };

@@ -7,7 +7,7 @@ library raises (``gdeconv._lib.EngineError``).
 Layouts: images fp32 [N,1,H,W] contiguous (NCHW, C=1, as in the reference); the OTF is the
 half spectrum stored transposed, complex64 [N, W//2+1, H] (``otf[g, kx, ky]``).
 
-Sizes: any H x W with 2 <= H, W <= 1638 (square or not).  Square 32/48/64/96/128/256 run the
+Sizes: any H x W with 2 <= H, W <= 4096 (square or not).  Square 32/48/64/96/128/256 run the
 compile-time-planned kernels (and the fused whole-galaxy kernels at 256^2 / <= 128); every other
 size runs the runtime-planned kernels of ``csrc/gd_generic.hpp`` with the same operation chains
 (``supported(H, W)`` returns 1 resp. 2).
@@ -107,7 +107,7 @@ def workspace(N, H, W, device):
     if nbytes is None:
         lib = _lib.load()
         if not lib.gd_supported_size(H, W):
-            raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 1638])")
+            raise ValueError(f"unsupported image size {H}x{W} (H and W must be in [2, 4096])")
         nbytes = _WS_BYTES[(N, H, W)] = max(16, int(lib.gd_workspace_bytes(max(N, 1), H, W)))
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
@@ -391,7 +391,7 @@ class GaussXState:
         nbytes = int(self.lib.gd_gx_state_bytes(N1, self.H, self.W))
         if nbytes == 0:
             raise ValueError(f"UnrolledADMMGaussian: unsupported image size {self.H}x{self.W} "
-                             "(even sides 2 .. 818: the 2x padded grid must fit the engine; the reference itself "
+                             "(even sides 2 .. 2048: the 2x padded grid must fit the engine; the reference itself "
                              "fails on odd sides, its crop_half(pad_double(.)) returning H - 1 rows)")
         with _on(self.dev):
             self.alpha, self.alpha_s = _galaxy_scalar(alpha, self.N, "alpha", self.dev)
@@ -572,7 +572,7 @@ class ADMMState:
         nbytes = ADMMState._state_bytes.get(skey)
         if nbytes is None:
             if not self.lib.gd_supported_size(self.H, self.W):
-                raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 1638])")
+                raise ValueError(f"unsupported image size {self.H}x{self.W} (H and W must be in [2, 4096])")
             nbytes = ADMMState._state_bytes[skey] = int(self.lib.gd_admm_state_bytes(max(self.N, 1), self.H, self.W,
                                                                                       self.llh))
         with _on(self.dev):

@@ -10,7 +10,7 @@
  *     No C++ exception crosses the ABI.  Re-entrant across streams given distinct workspaces;
  *   - spectra are half spectra stored TRANSPOSED, complex64 [N][W/2+1][H] (kx-major, ky
  *     contiguous); `ws` is a workspace of gd_workspace_bytes(N, H, W) bytes;
- *   - sizes: any H x W with 2 <= H, W <= 1638 (utils/utils_torch.py's torch.fft path takes any size);
+ *   - sizes: any H x W with 2 <= H, W <= 4096 (utils/utils_torch.py's torch.fft path takes any size);
  *     square 32/48/64/96/128/256 run compile-time-planned kernels, every other size the runtime-
  *     planned ones (csrc/gd_generic.hpp) with the same operation chains.  The Gaussian ADMM init and
  *     iteration run one launch per call at 256^2 (k_gal_reg_init / k_gal_reg), 32/48/64 (k_gal_small*)
@@ -157,7 +157,7 @@ int gd_filter_power(const float* filt, float* power_half, int N, int H, int W, v
 int gd_filter_power_taps(const int* rc, const float* vals, int ntaps, float* power_half, int H, int W,
                          void* stream);
 
-/* UnrolledADMMGaussian (the variant train.py trains): images H x W (both even, <= 818, square or not:
+/* UnrolledADMMGaussian (the variant train.py trains): images H x W (both even, <= 2048, square or not:
  * a non-square image runs on the runtime-planned kernels) and PSFs of the SAME size, zero-padded per
  * axis to the 2H x 2W grid (pad_double) with the reference's
  * ifftshift / fftshift / crop_half expressed as origin placement (the shift is a common phase that

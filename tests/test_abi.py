@@ -52,10 +52,11 @@ def test_host_only_queries(lib):
     from gdeconv import _lib as _lib_mod
     assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 5
     assert lib.gd_supported_size(256, 256) == 1 and lib.gd_supported_size(48, 48) == 1
-    # other sizes up to 1638 per side, square or not, run the runtime-planned kernels (2)
+    # other sizes up to 4096 per side, square or not, run the runtime-planned kernels (2)
     assert lib.gd_supported_size(50, 50) == 2 and lib.gd_supported_size(256, 128) == 2
     assert lib.gd_supported_size(48, 1025) == 2 and lib.gd_supported_size(1638, 1200) == 2
-    assert lib.gd_supported_size(1, 48) == 0 and lib.gd_supported_size(48, 1639) == 0
+    assert lib.gd_supported_size(1639, 48) == 2 and lib.gd_supported_size(4096, 4096) == 2
+    assert lib.gd_supported_size(1, 48) == 0 and lib.gd_supported_size(48, 4097) == 0
     # workspace: N * 2 images * (W/2+1) * H complex64
     assert lib.gd_workspace_bytes(4096, 256, 256) == 4096 * 2 * 129 * 256 * 8
     assert lib.gd_otf_bytes(2, 48, 48) == 2 * 25 * 48 * 8
@@ -92,7 +93,7 @@ def test_argument_errors_need_no_device(lib):
     # validation happens before any HIP call: odd PSF, unsupported size, bad llh
     assert lib.gd_psf_to_otf(None, 0, 5, 5, 1, 48, 48, None, None, None) == -1
     assert b"even" in lib.gd_last_error()
-    assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 4096, 50, None, None) == -2
+    assert lib.gd_conv_fft_batch(None, 0, None, None, 1, 4097, 50, None, None) == -2
     assert lib.gd_admm_init(None, None, 0, 48, 48, None, 0, None, 0, 7, 1, 48, 48,
                             None, None, None, None) == -1
     # state: Gaussian |H|^2 (fp32) + conj(H)F(y/a) + F(u1) + conj(H)F(v-u2); Poisson OTF + two images

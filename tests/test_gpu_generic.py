@@ -1,6 +1,7 @@
 """GPU parity of the runtime-planned path (csrc/gd_generic.hpp): image sizes outside the compile-time
 set (square 32/48/64/96/128/256), square or not, odd, prime, up to 1024 per side - against the
-reference's golden vectors (tests/golden/make_golden_sizes.py) and the oracle.
+reference's golden vectors (tests/golden/make_golden_sizes.py) and the oracle; up to 4096 per side against the fp64
+oracle (lines longer than 1638 points take the CU's whole 160 KiB of LDS).
 Bar: per galaxy max|out - ref| <= 1e-5 * max|ref| (fp32)."""
 import numpy as np
 import pytest
@@ -14,7 +15,8 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-5
 SIZES = [(40, 40), (64, 48), (45, 60), (97, 80), (192, 160), (45, 61), (255, 255)]   # sizes.npz (odd W last)
 FFT_SIZES = [(2, 2), (3, 5), (17, 19), (40, 40), (64, 48), (45, 60), (97, 80), (243, 125), (1000, 30),
-             (7, 1024), (1024, 1024), (96, 256), (256, 255), (1638, 1200), (1536, 1638), (1025, 1637)]
+             (7, 1024), (1024, 1024), (96, 256), (256, 255), (1638, 1200), (1536, 1638), (1025, 1637),
+             (1639, 1640), (2053, 3000), (4096, 4096)]   # lines > 1638: the 160 KiB LDS budget (round 6)
 
 
 def T(a):
@@ -309,6 +311,45 @@ def test_generic_large_images_admm_and_wiener(dev, H, W):
     e = nerr(out, ref)
     print(f"{H}x{W}: Wiener / ADMM(2) vs fp64 oracle, ADMM {e:.2e}")
     assert e < TOL
+
+
+@pytest.mark.parametrize("H,W", [(4096, 4096), (2053, 2500)])
+def test_generic_big_lines_wiener_rl_admm(dev, H, W):
+    """Lines longer than 1638 points (up to 4096: the whole 160 KiB of a CU's LDS per workgroup, dynamic LDS above
+    64 KiB allowed per kernel): Wiener, Richardson-Lucy(3) and Unrolled_ADMM(2, Gaussian) with an identity denoiser
+    against the fp64 oracle; 2053 is prime (one odd-prime DFT stage of 2053 points)."""
+    from gdeconv import engine
+    from gdeconv.synth import make_batch
+    obs, psf, alpha, _ = make_batch(1, H, W, h=48, seed=H + 3 * W)
+    wien = engine.wiener(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    assert report(f"Wiener {H}x{W}", wien, O.wiener(obs.double(), psf.double(), alpha.double())) < TOL
+    rl = engine.richardson_lucy(obs.to(dev), psf.to(dev), 3).cpu()
+    assert report(f"Richardson-Lucy(3) {H}x{W}", rl, O.richardson_lucy(obs.double(), psf.double(), 3)) < TOL
+    rho1 = torch.full((1, 1, 1, 2), 0.9)
+    rho2 = torch.full((1, 1, 1, 2), 1.1)
+    m = _spectral_model(2, "Gaussian", dev, rho1, rho2)
+    with torch.no_grad():
+        out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+    ref = O.admm_forward(obs.double(), psf.double(), alpha.double(), rho1.double(), rho2.double(), "Gaussian")
+    assert report(f"Unrolled_ADMM(2) identity {H}x{W}", out, ref) < TOL
+
+
+def test_generic_gauss2x_big_grid(dev):
+    """UnrolledADMMGaussian beyond round 5's 818 cap: 1024 x 1024 images on the 2048 x 2048 padded grid (lines longer
+    than 1638 points), init_l2 and one X update against the fp64 oracle (models/unrolled_admm_gaussian.py:89-93)."""
+    from gdeconv import engine
+    from gdeconv.synth import make_batch
+    obs, psf, alpha, _ = make_batch(1, 1024, h=1024, seed=21, device=dev)
+    st = engine.GaussXState(obs, psf, alpha)
+    _, Y, Ht, HtH = O.gx_spectra(obs.cpu().double(), psf.cpu().double())
+    z0 = st.init().cpu()
+    assert report("UnrolledADMMGaussian init_l2 1024x1024", z0, O.gx_init_l2(Y, Ht, HtH, alpha.cpu().double())) < TOL
+    gen = torch.Generator().manual_seed(3)
+    z, u = (torch.randn(obs.shape, generator=gen) for _ in range(2))
+    rho = torch.tensor([0.8]).view(1, 1, 1, 1)
+    x = engine.gx_x_update(st, z.to(dev), u.to(dev), rho.to(dev)).cpu()
+    ref = O.gx_x_update(Y, Ht, HtH, z.double(), u.double(), rho.double())
+    assert report("UnrolledADMMGaussian X update 1024x1024", x, ref) < TOL
 
 
 @pytest.mark.parametrize("L,llh", [(48, "Poisson"), (80, "Poisson"), (80, "Gaussian"), (144, "Gaussian")])

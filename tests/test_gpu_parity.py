@@ -556,8 +556,8 @@ def test_errors_are_loud(eng, dev):
     with pytest.raises(EngineError):
         eng.psf_to_otf_half(torch.rand(1, 1, 64, 64, device=dev), 1, 48, 48)  # PSF > image
     with pytest.raises((EngineError, ValueError)):
-        eng.conv_half(torch.zeros(1, 851, 4, dtype=torch.complex64, device=dev),
-                      torch.rand(1, 1, 4, 1700, device=dev))                  # unsupported size (W > 1638)
+        eng.conv_half(torch.zeros(1, 2051, 4, dtype=torch.complex64, device=dev),
+                      torch.rand(1, 1, 4, 4100, device=dev))                  # unsupported size (W > 4096)
     with pytest.raises(ValueError):
         eng.wiener(x.cpu(), torch.rand(1, 1, 48, 48), torch.ones(1))          # CPU tensors
     assert eng.conv_half(eng.empty_otf(0, 48, 48, dev), torch.empty(0, 1, 48, 48, device=dev)).shape[0] == 0
