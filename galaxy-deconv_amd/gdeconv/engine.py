@@ -598,9 +598,9 @@ class ADMMState:
     _reads_rho = {}     # (H, W, llh) -> forced gd_admm_init_reads_rho (overrides for tests; empty by default)
     _state_bytes = {}   # (N, H, W, llh) -> gd_admm_state_bytes (pure in its arguments)
     # (device index, main stream) -> (side stream, fork event, join event) of init_concurrent (LRU, bounded).  The fork
-    # and join go through these persistent events, not Stream.wait_stream's temporary ones: an event recorded during
-    # a capture on the side stream (which itself forks the engine's capture streams) and destroyed before
-    # hipStreamEndCapture is what crashed the ROCm 7 runtime there (tools/capture_probe.hip mode 11)
+    # and join go through these persistent events rather than Stream.wait_stream's temporary ones (one event pair per
+    # side stream, no event created or destroyed per forward; whether the events are temporary made no difference to
+    # the ROCm 7.0 capture crash, profiles/r06_capture_rootcause.txt)
     _side_streams = {}
     _SIDE_STREAMS_MAX = 16
 
