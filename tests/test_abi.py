@@ -48,6 +48,17 @@ def test_library_exports_every_header_symbol(lib):
         assert len(SIGNATURES[name][1]) == nargs, f"{name}: header has {nargs} args"
 
 
+def test_hip_runtime_version_is_torchs(lib):
+    """In a PyTorch process the engine runs on the HIP runtime PyTorch bundles (same soname), not /opt/rocm's: the
+    version gdeconv's capture guard reads (gd_hip_runtime_version) is torch.version.hip's."""
+    import torch
+    v = lib.gd_hip_runtime_version()
+    assert v > 0
+    if torch.version.hip:
+        major, minor, patch = (int(x) for x in torch.version.hip.split(".")[:3])
+        assert v == major * 10_000_000 + minor * 100_000 + patch
+
+
 def test_host_only_queries(lib):
     from gdeconv import _lib as _lib_mod
     assert lib.gd_abi_version() == _lib_mod.ABI_VERSION == 5
