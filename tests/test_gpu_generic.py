@@ -320,18 +320,25 @@ def test_generic_big_lines_wiener_rl_admm(dev, H, W):
     against the fp64 oracle; 2053 is prime (one odd-prime DFT stage of 2053 points)."""
     from gdeconv import engine
     from gdeconv.synth import make_batch
-    obs, psf, alpha, _ = make_batch(1, H, W, h=48, seed=H + 3 * W)
+    # 2053 x 2500: two galaxies, so the chunked pipeline (one galaxy per 96 MiB chunk here) runs its two streams
+    obs, psf, alpha, _ = make_batch(1 if H == 4096 else 2, H, W, h=48, seed=H + 3 * W)
     wien = engine.wiener(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
     assert report(f"Wiener {H}x{W}", wien, O.wiener(obs.double(), psf.double(), alpha.double())) < TOL
     rl = engine.richardson_lucy(obs.to(dev), psf.to(dev), 3).cpu()
     assert report(f"Richardson-Lucy(3) {H}x{W}", rl, O.richardson_lucy(obs.double(), psf.double(), 3)) < TOL
-    rho1 = torch.full((1, 1, 1, 2), 0.9)
-    rho2 = torch.full((1, 1, 1, 2), 1.1)
+    rho1 = torch.full((obs.shape[0], 1, 1, 2), 0.9)
+    rho2 = torch.full((obs.shape[0], 1, 1, 2), 1.1)
     m = _spectral_model(2, "Gaussian", dev, rho1, rho2)
     with torch.no_grad():
         out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
     ref = O.admm_forward(obs.double(), psf.double(), alpha.double(), rho1.double(), rho2.double(), "Gaussian")
     assert report(f"Unrolled_ADMM(2) identity {H}x{W}", out, ref) < TOL
+    if H != 4096:  # the Poisson chain (V step per pixel in the row-inverse kernel) at a prime side
+        m = _spectral_model(2, "Poisson", dev, rho1, rho2)
+        with torch.no_grad():
+            out = m(obs.to(dev), psf.to(dev), alpha.to(dev)).cpu()
+        ref = O.admm_forward(obs.double(), psf.double(), alpha.double(), rho1.double(), rho2.double(), "Poisson")
+        assert report(f"Unrolled_ADMM(2, Poisson) identity {H}x{W}", out, ref) < TOL
 
 
 def test_generic_gauss2x_big_grid(dev):
