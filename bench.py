@@ -400,7 +400,8 @@ def main():
     if world == 1 and not args.no_extra and args.workload == "admm" and args.size == 256 and args.llh == "Gaussian":
         for key, over in (("configs1", dict(batch=256, size=48, n_iters=8, steps=max(200, args.steps),
                                             warmup=max(20, args.warmup), settle_s=0.5, no_ingest=True,
-                                            no_e2e=True, cpu_sample=64)),
+                                            e2e_sample=256, e2e_forwards=max(10, args.e2e_forwards),
+                                            cpu_sample=64)),
                           ("configs4", dict(workload="rl", batch=4096, size=256, n_iters=100, steps=args.steps,
                                             warmup=min(2, args.warmup), settle_s=1.0, no_ingest=True, no_e2e=True,
                                             no_graph=True, cpu_sample=4))):
@@ -783,6 +784,24 @@ def measure(args, ctx):
                              "frac_of_fp32_ceiling": gal_e2e * flop_gal / (FP32_PEAK_TFLOPS * 1e12),
                              "sample": f"{G} galaxies, full model with PyTorch ResUNet (fp32, MIOpen, NHWC), "
                                        f"{args.e2e_forwards} timed forwards after one warm forward"}
+        if L <= 64 and not args.no_graph:
+            # small stamps: the host's ~60 launches per forward set the eager pace; the whole model (ResUNet included)
+            # replayed as one hipGraph (gdeconv.graphs.GraphedForward, the serving path of SURVEY 8(f) rank 2)
+            from gdeconv.graphs import GraphedForward
+            gf = GraphedForward(model, o2, p2, a2)
+            gf.replay()
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            for _ in range(args.e2e_forwards):
+                gf.replay()
+            torch.cuda.synchronize()
+            tg = time.perf_counter() - tg
+            gal_g = G * args.e2e_forwards / tg
+            rec["end_to_end"]["graphed"] = {"value": gal_g, "unit": "galaxies/s",
+                                            "ms_per_forward": tg * 1e3 / args.e2e_forwards,
+                                            "frac_of_fp32_ceiling": gal_g * flop_gal / (FP32_PEAK_TFLOPS * 1e12),
+                                            "note": "the same sample's forward captured once (GraphedForward) and replayed"}
+            del gf
         del o2, p2, a2
     if world > 1:
         dist.barrier()   # every rank's GPU work and collectives are done before rank 0 loads the host cores
