@@ -2852,7 +2852,7 @@ int gd_abi_version(void) { return GD_ABI_VERSION; }
 
 // bumped whenever a kernel's memory traffic changes; PMC summaries are stamped with it so a stale
 // profile is never reported against a different engine
-const char* gd_engine_rev(void) { return "r06.1"; }
+const char* gd_engine_rev(void) { return "r06.2"; }
 
 // the source hash __graft_entry__.build() computed (gdeconv._lib.source_hash); the "gdsrc:" marker lets the
 // build find it in the binary without loading it

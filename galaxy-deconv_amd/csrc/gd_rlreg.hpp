@@ -20,7 +20,7 @@
 
 #ifndef GD_RL_HPF
 #define GD_RL_HPF 4  // bit 0 / bit 1: slice A's / B's OTF columns loaded before its forward column FFTs (latency hidden);
-                      // bit 2: slice A's column 0 before the FFTs, column 1 right after them; bit 3 (with 2): the Nyquist bins too
+                      // bit 2: slice A's column 0 before the FFTs, column 1 right after them
 #endif
 #ifndef GD_RL_DPP
 #define GD_RL_DPP 0  // 1: every line FFT transposes in registers (DPP) instead of through the LDS exchange
@@ -31,6 +31,7 @@
 #ifndef GD_RL_FASTDIV
 #define GD_RL_FASTDIV 1
 #endif
+
 // y / Hx without the IEEE division sequence (div_scale / div_fmas / div_fixup and denorm-mode toggles,
 // ~10 instructions): reciprocal, then one Newton correction of the quotient (within an ulp of the
 // division; the pixel loop runs 256 of these per lane per iteration)
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
     __shared__ float2 tw[L];
     __shared__ __attribute__((aligned(16))) float2 S[RG::U];
     __shared__ float2 nyq[RG::NP];  // X_p[L/2] of every pair
-    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum, then its product
+    __shared__ float2 nyqc[L];      // the Nyquist column's spectrum (line 0's own bins)
     __shared__ float nyqo[L];       // the Nyquist column after the inverse (x(., L/2))
     const int tid0 = threadIdx.x;
     const int g = blockIdx.x;
@@ -59,6 +60,12 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
     const float* yg = a.y + (size_t)g * L * L;
     float* xg = a.o0 + (size_t)g * L * L;
     const float2* Hg = a.otf + (size_t)g * K * L;
+    // the OTF's Nyquist column (kx = L/2), constant over the iterations: read once into LDS, so that line 0 - the
+    // only holder of that column's bins - forms its products alone (round 6: the two workgroup barriers and the
+    // per-pass global loads of a four-wave product are gone, 121.9 -> 120.0 ms per 4096 x RL(100), bit-identical;
+    // profiles/r06zj_rl_nyquist_ab.txt)
+    __shared__ float2 hnyq[L];
+    for (int e = tid0; e < L; e += T) hnyq[e] = Hg[(size_t)(L / 2) * L + e];
     const float div = Hg[0].x;  // conv(Ht, ones) = H(0, 0)
     const float idiv = 1.0f / div;
     const int tid = tid0;
@@ -170,11 +177,6 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
             static_assert(RG::CPL == 2, "two columns per line and slice");
             float2 hA0[F2];  // column 0's OTF, in flight during the FFTs
             hload(hA0, line);
-#if GD_RL_HPF & 8
-            const bool nq = __builtin_amdgcn_readfirstlane(tt >> 6) < L / 64;
-            float2 hn4 = make_float2(0.f, 0.f);  // the Nyquist bin's OTF too
-            if (nq) hn4 = Hg[(size_t)(L / 2) * L + opaque(tt)];
-#endif
             __builtin_amdgcn_sched_barrier(0);
 #endif
             if constexpr ((GD_RL_PAIR & 1) != 0) {
@@ -221,21 +223,18 @@ __global__ __launch_bounds__(512) void k_rl_reg(Args a, int n_iters) {
                 __builtin_amdgcn_sched_barrier(0);
             }
 #endif
-            lds_barrier();  // nyqc complete
-            if (__builtin_amdgcn_readfirstlane(tt >> 6) < L / 64) {
-#if GD_RL_HPF & 8
-                const float2 hn = hn4;
-#else
-                const float2 hn = Hg[(size_t)(L / 2) * L + tt];
-#endif
-                nyqc[tt] = CONJ ? cmulc(nyqc[tt], hn) : cmul(nyqc[tt], hn);
-            }
-            lds_barrier();  // Nyquist products
+            __builtin_amdgcn_sched_barrier(0);
+            if (l0) {  // the lane's own Nyquist bins (written by the split above), times the column's OTF
 #pragma unroll
-            for (int s = 0; s < F2; ++s) {
-                const float2 cn = nyqc[j + F1 * s];
-                if (l0) CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
+                for (int s = 0; s < F2; ++s) {
+                    const int ky = j + F1 * s;
+                    const float2 hn = hnyq[ky];
+                    const float2 cn = CONJ ? cmulc(nyqc[ky], hn) : cmul(nyqc[ky], hn);
+                    CA[0][s] = make_float2(CA[0][s].x - cn.y, CA[0][s].y + cn.x);
+                    if (s % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // four bins' reads in flight at a time
+                }
             }
+            __builtin_amdgcn_sched_barrier(0);
             if constexpr ((GD_RL_PAIR & 1) != 0) {
                 reg_fft2<L, true>(CA[0], CA[1], opaque(j), my, tw);
                 pin(CA[0]);
