@@ -659,11 +659,18 @@ struct GLaunch {
     static std::string nm(const char* k, int mode, const Dims& d) {
         return std::string(k) + "<" + std::to_string(d.H) + "x" + std::to_string(d.W) + "," + std::to_string(mode) + ">";
     }
-    // dynamic LDS above 64 KiB (lines longer than kSmallLen) must be allowed per kernel before its launch
+    // dynamic LDS above 64 KiB (lines longer than kSmallLen) must be allowed per kernel before its launch; set once
+    // per kernel and size (normally at an eager call, before any stream capture of the same operation)
     static int allow_lds(const void* k, size_t bytes) {
         if (bytes <= 65536) return GD_OK;
+        static std::mutex mu;
+        static std::map<const void*, size_t> allowed;
+        std::lock_guard<std::mutex> lk(mu);
+        size_t& have = allowed[k];
+        if (have >= bytes) return GD_OK;
         if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
             return fail(GD_ERR_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+        have = bytes;
         return GD_OK;
     }
     static int row_grid(int NI, const Args& a, const Dims& d) {

@@ -79,6 +79,19 @@ def test_graphed_forward_chunked_pipeline(dev, H, W, mode):
         lib.gd_set_capture_pipeline(old_mode)
 
 
+def test_graphed_forward_big_lines(dev):
+    """Lines longer than 1638 points (dynamic LDS above 64 KiB, allowed per kernel at the eager warm-up): a 1700 x 1800
+    forward captured and replayed bit-identically to the eager one."""
+    from gdeconv.graphs import GraphedForward
+    from gdeconv.synth import make_batch
+    m = _model(2, "Gaussian", dev, identity=True)
+    obs, psf, alpha, _ = make_batch(1, 1700, 1800, seed=17, device=dev)
+    with torch.no_grad():
+        eager = m(obs, psf, alpha)
+    g = GraphedForward(m, obs, psf, alpha, clone=True)
+    assert torch.equal(g(obs, psf, alpha), eager)
+
+
 def test_graphed_forward_side_stream_chunked_init(dev):
     """The round-4 capture crash's shape, scaled down: a batch large enough for the init to run on a side stream
     beside the SubNet (models.CONCURRENT_INIT_PIXELS), the chunked runtime-planned Gaussian init (fused init off)
